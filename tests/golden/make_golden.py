@@ -1,0 +1,205 @@
+"""Generate the golden fixtures in tests/golden/ by running the REFERENCE's own source.
+
+Run in the development container (the only place /root/reference exists):
+
+    python tests/golden/make_golden.py
+
+What is pinned and what is not
+------------------------------
+The reference (lizaibeim/mmla-audio) has no tests and no golden vectors.  This script
+executes the reference's own Python source files -- read as text from /root/reference and compiled
+here, never their cached bytecode -- with the third-party modules that are absent from this image
+(librosa, python_speech_features, tensorflow, webrtcvad, pydub) replaced by stubs.  The librosa /
+psf stubs call the numpy restatements in ``oracle/``.  Real matplotlib (3.10) and PIL encode and
+decode the PNG, and real scipy reads the WAV files.  So the fixtures pin:
+
+  * the reference glue: pad/trunc (overlap_features_generator.py:73-80,94-98), normalize_matrix
+    (:103-117), the RGB assembly loop (:139-146), ``plt.imsave(origin="lower")`` quantisation
+    (:151) + ``decode_png(...,3)`` (record_on_pc.py:156-158), ``input_feature_gen``
+    (speaker_identification.py:372-398) incl. the 'silent' gate and 256-frame pad/trunc, and
+    ``delta`` (:141-151);
+  * NOT the librosa / psf arithmetic underneath (parity unpinned; no reference vector exists).
+
+numpy note: this image has numpy 2.2 (NEP 50 promotion).  Under the reference's pinned numpy 1.21
+``1 - np.float32(x)`` in the assembly loop is float64; here it is float32.  The PNG fixture
+therefore differs from the numpy-1.21 result in at most a few pixels by 1 LSB where 1-x sits on a
+quantisation edge (tests allow that, see tests/test_oracle_golden.py).
+
+Output: tests/golden/od_golden.npz, si_golden.npz (small, compressed).
+"""
+import io
+import os
+import sys
+import tempfile
+import types
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = '/root/reference'
+sys.path.insert(0, REPO)
+
+from oracle import od_fe, si_fe, synth  # noqa: E402
+
+
+class _Anything:
+    """Permissive stand-in for tensorflow/keras symbols the reference only references at import."""
+
+    def __init__(self, *a, **k):
+        pass
+
+    def __call__(self, *a, **k):
+        return _Anything()
+
+    def __getattr__(self, name):
+        return _Anything()
+
+
+def _module(name, **attrs):
+    m = types.ModuleType(name)
+    m.__dict__.update(attrs)
+    m.__getattr__ = lambda n: _Anything()
+    sys.modules[name] = m
+    return m
+
+
+def _install_stubs():
+    import scipy.io.wavfile as wavfile
+
+    def load(path, sr=None):
+        assert sr is None
+        rate, x = wavfile.read(path)
+        assert x.dtype == np.int16
+        return od_fe.load_int16(x), rate
+
+    def melspectrogram(y, sr, hop_length, n_fft, n_mels):
+        return od_fe.melspectrogram(y, sr=sr, hop_length=hop_length, n_fft=n_fft, n_mels=n_mels)
+
+    def power_to_db(s, ref):
+        assert ref is np.max
+        return od_fe.power_to_db(s)
+
+    def zero_crossing_rate(y, frame_length, hop_length):
+        return od_fe.zero_crossing_rate(y, frame_length=frame_length, hop_length=hop_length)
+
+    feature = _module('librosa.feature', melspectrogram=melspectrogram,
+                      zero_crossing_rate=zero_crossing_rate)
+    _module('librosa', load=load, feature=feature, power_to_db=power_to_db,
+            mel_frequencies=od_fe.mel_frequencies)
+
+    def mfcc(sig, rate, winlen, winstep, nfft):
+        assert (rate, winlen, winstep, nfft) == (16000, 0.025, 0.01, 512)
+        return si_fe.mfcc(sig, rate)
+
+    _module('python_speech_features', mfcc=mfcc)
+    _module('webrtcvad', Vad=_Anything)
+    _module('pydub', AudioSegment=_Anything)
+
+    class Callback:
+        def __init__(self, *a, **k):
+            pass
+
+    tf = _module('tensorflow')
+    keras = _module('tensorflow.keras')
+    tf.keras = keras
+    for sub in ('backend', 'regularizers', 'layers', 'metrics', 'models', 'optimizers'):
+        setattr(keras, sub, _module('tensorflow.keras.' + sub))
+    keras.callbacks = _module('tensorflow.keras.callbacks', Callback=Callback, EarlyStopping=_Anything)
+
+
+def _load_reference(relpath, modname):
+    """Compile a reference source file from its text (no __pycache__ is read or written)."""
+    path = os.path.join(REF, relpath)
+    src = open(path).read()
+    mod = types.ModuleType(modname)
+    mod.__file__ = path
+    code = compile(src, path, 'exec', dont_inherit=True)
+    exec(code, mod.__dict__)
+    return mod
+
+
+def _write_wav(path, pcm):
+    import scipy.io.wavfile as wavfile
+    wavfile.write(path, 16000, np.asarray(pcm, dtype=np.int16))
+
+
+def _png_rgb(path):
+    from PIL import Image
+    return np.asarray(Image.open(path).convert('RGB'), dtype=np.uint8)
+
+
+OD_CASES = [
+    # (name, pcm generator)
+    ('voiced_2p5s', lambda: synth.clip(0, 40000)),
+    ('overlap_2p5s', lambda: synth.clip(1, 40000)),
+    ('noise_2p56s', lambda: synth.clip(2, 40960)),
+    ('near_silence', lambda: synth.clip(3, 40000)),          # class 3: +-1 LSB
+    ('digital_zeros', lambda: synth.clip(8, 40000)),         # class 3: zeros -> NaN image (diff=0)
+    ('clipped', lambda: synth.clip(4, 40000)),
+    ('short_1s_zero_pad', lambda: synth.clip(5, 16000)),     # < 24000: zero-padded (:73-76)
+    ('exact_1p5s', lambda: synth.clip(6, 24000)),
+]
+
+SI_CASES = [
+    ('voiced_1p5s', lambda: synth.clip(10, 24000)),         # 149 frames -> pad 256
+    ('overlap_2p56s', lambda: synth.clip(11, 40960)),       # 255 frames
+    ('noise_2p5s', lambda: synth.clip(12, 40000)),          # 249 frames
+    ('long_3s_trunc', lambda: synth.clip(14, 48000)),       # 299 frames -> truncate to 256
+    ('short_0p3s', lambda: synth.clip(15, 4800)),           # 29 frames
+    ('silent_3999', lambda: synth.clip(16, 3999)),          # < 4000 -> 'silent'
+    ('edge_4000', lambda: synth.clip(17, 4000)),            # exactly 4000 -> features
+    ('zeros_1p5s', lambda: np.zeros(24000, np.int16)),      # log(eps) path
+]
+
+
+def main():
+    _install_stubs()
+    ofg_mod = _load_reference('OverlapDetection/scripts/overlap_features_generator.py', 'ref_ofg')
+    si_mod = _load_reference('SpeakerIdentification/scripts/speaker_identification.py', 'ref_si')
+    ofg = ofg_mod.OverlapFeaturesGenerator(wl=25, hl=10)
+    assert ofg.get_attributes() == (400, 160, 16000)
+
+    tmp = tempfile.mkdtemp(prefix='mmla_golden_')
+    od = {'names': np.array([c[0] for c in OD_CASES])}
+    for i, (name, gen) in enumerate(OD_CASES):
+        pcm = gen()
+        wav = os.path.join(tmp, f'od{i}.wav')
+        _write_wav(wav, pcm)
+        s_db, norm = ofg.generate_mels(wav)
+        zcr = ofg.generate_zcr(wav)
+        img = ofg.generate_zcr_image(wav, tmp + '/', None)
+        ofg.generate_zcr_image(wav, tmp + '/', f'od{i}.png')
+        png = _png_rgb(os.path.join(tmp, f'od{i}.png'))
+        od[f'pcm_{i}'] = pcm
+        od[f'db_{i}'] = np.asarray(s_db, np.float32)
+        od[f'norm_{i}'] = np.asarray(norm, np.float32)
+        od[f'zcr_{i}'] = np.asarray(zcr, np.float64)
+        od[f'png_{i}'] = png
+        if i == 0:
+            od['image_0'] = np.asarray(img, np.float64)
+        print('OD', name, s_db.shape, norm.dtype, zcr.shape, png.shape)
+
+    si = {'names': np.array([c[0] for c in SI_CASES])}
+    for i, (name, gen) in enumerate(SI_CASES):
+        pcm = gen()
+        wav = os.path.join(tmp, f'si{i}.wav')
+        _write_wav(wav, pcm)
+        x = si_mod.input_feature_gen(wav)
+        si[f'pcm_{i}'] = pcm
+        si[f'silent_{i}'] = np.array(isinstance(x, str) and x == 'silent')
+        si[f'feat_{i}'] = np.zeros((1, 256, 39)) if isinstance(x, str) else np.asarray(x, np.float64)
+        print('SI', name, 'silent' if isinstance(x, str) else x.shape)
+    rng = np.random.default_rng(7)
+    dx = rng.standard_normal((37, 13))
+    si['delta_in'] = dx
+    si['delta_out'] = si_mod.delta(dx, 2)
+    si['delta2_out'] = si_mod.delta(si_mod.delta(dx, 2), 2)
+
+    np.savez_compressed(os.path.join(HERE, 'od_golden.npz'), **od)
+    np.savez_compressed(os.path.join(HERE, 'si_golden.npz'), **si)
+    print('wrote', os.path.join(HERE, 'od_golden.npz'), os.path.join(HERE, 'si_golden.npz'))
+
+
+if __name__ == '__main__':
+    main()
