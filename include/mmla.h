@@ -1,0 +1,159 @@
+/*
+ * mmla.h -- C ABI of the MI355X-native mmla-audio hot path (libmmla.so).
+ *
+ * The reference (lizaibeim/mmla-audio) has no FFI of its own: its per-clip path is a set of plain
+ * Python functions over librosa / python_speech_features / TensorFlow.  Each entry
+ * point below replaces one of those call sites; the Python drop-in shim (mmla_audio_amd/) binds them
+ * with ctypes under the reference's own names (INTEGRATION.md shows the binding).
+ *
+ * Conventions
+ *   - Every function returns MMLA_OK (0) or a negative MMLA_E_* code; the message is in
+ *     mmla_last_error(ctx).  Nothing throws across the ABI.
+ *   - Buffers are caller-owned.  By default they are HOST pointers (the call copies in and out and
+ *     is synchronous).  With MMLA_DEVICE_PTR they are device pointers on the context's GPU and the
+ *     call only enqueues work on the context stream (mmla_set_stream), returning immediately.
+ *   - A context is not thread-safe: use one per thread / per GPU.  The multi-GPU driver (one process
+ *     per GPU, RCCL all-gather of logits) lives above this ABI.
+ *   - PCM is 16 kHz mono int16; clip c starts at pcm + c * clip_stride (in samples) and has
+ *     lens[c] valid samples (lens == NULL: every clip has clip_len samples).
+ */
+#ifndef MMLA_H_
+#define MMLA_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MMLA_ABI_VERSION 1
+
+enum mmla_status {
+  MMLA_OK = 0,
+  MMLA_E_INVALID = -1,   /* bad argument (null pointer, negative size, unknown model kind) */
+  MMLA_E_HIP = -2,       /* HIP runtime error */
+  MMLA_E_NOWEIGHTS = -3, /* forward called before mmla_load_weights for that model */
+  MMLA_E_OOM = -4,       /* device allocation failed */
+  MMLA_E_SHAPE = -5      /* packed weight blob has the wrong number of floats */
+};
+
+enum mmla_model { MMLA_MODEL_OD = 0, MMLA_MODEL_SI = 1 };
+enum mmla_head { MMLA_HEAD_SOFTMAX = 0, MMLA_HEAD_SIGMOID = 1 };
+
+#define MMLA_DEVICE_PTR 0x1u /* data pointers are device pointers; call is asynchronous */
+
+/* OD front-end geometry (overlap_features_generator.py:39-42,73-81) */
+#define MMLA_OD_MELS 128
+#define MMLA_OD_FRAMES 151
+#define MMLA_OD_CLIP 24000
+/* SI front-end geometry (speaker_identification.py:386-395) */
+#define MMLA_SI_FRAMES 256
+#define MMLA_SI_DIMS 39
+#define MMLA_SI_SILENT_LEN 4000
+
+typedef struct mmla_ctx mmla_ctx;
+
+int mmla_abi_version(void);
+
+/* Create a context on HIP device `device` (owns a stream, device workspaces and loaded weights). */
+int mmla_create(int device, mmla_ctx** out);
+int mmla_destroy(mmla_ctx* ctx);
+const char* mmla_last_error(const mmla_ctx* ctx);
+/* Use an external hipStream_t (e.g. torch.cuda.current_stream().cuda_stream); NULL = own stream. */
+int mmla_set_stream(mmla_ctx* ctx, void* hip_stream);
+int mmla_synchronize(mmla_ctx* ctx);
+/* Cap the clips processed per internal micro-batch (activation memory); 0 = default. */
+int mmla_set_microbatch(mmla_ctx* ctx, int64_t od_clips, int64_t si_clips);
+
+/*
+ * Load network weights from the packed float32 blob (host memory) in the canonical order of
+ * mmla_audio_amd/weights.py spec(): ascending Keras `layer_with_weights-k`; conv/dense = kernel,
+ * bias; BatchNorm = gamma, beta, moving_mean, moving_variance; Bidirectional LSTM = forward
+ * kernel, recurrent_kernel, bias, backward kernel, recurrent_kernel, bias.  Keras layouts.
+ * Replaces tf.keras.models.load_model(...) (record_on_pc.py:88; SI record_on_pc.py:77).
+ * n_classes: OD must be 2; SI = 630 (base model) or N speakers (deployed head).
+ * head: MMLA_HEAD_SOFTMAX (base Dense(630, softmax), speaker_identification.py:215) or
+ *       MMLA_HEAD_SIGMOID (deployed customized_dense, speaker_identification.py:409).
+ */
+int mmla_load_weights(mmla_ctx* ctx, int model_kind, const float* packed, int64_t n_floats,
+                      int32_t n_classes, int32_t head);
+
+/*
+ * OverlapDetection front-end, replaces OverlapFeaturesGenerator.generate_mels / generate_zcr /
+ * generate_zcr_image + the PNG round trip (overlap_features_generator.py:65-151;
+ * record_on_pc.py:156-158).  Per clip (first 24000 samples, zero-padded if shorter):
+ *   db      [n,128,151] f32  power_to_db(melspectrogram, ref=max, top_db=80)   (nullable)
+ *   norm_db [n,128,151] f32  normalize_matrix(db) in [0,1] (NaN for digital silence) (nullable)
+ *   zcr     [n,151]     f32  zero_crossing_rate(frame 400, hop 160)                 (nullable)
+ *   img     [n,128,151,3] u8 the decoded PNG the model reads: rows flipped
+ *                            (origin="lower"), R = trunc(255*zcr), G = B = trunc(255*(1-norm))
+ *                                                                                   (nullable)
+ */
+int mmla_od_features(mmla_ctx* ctx, const int16_t* pcm, int64_t n_clips, int64_t clip_stride,
+                     const int32_t* lens, int32_t clip_len, float* db, float* norm_db, float* zcr,
+                     uint8_t* img, uint32_t flags);
+
+/*
+ * SpeakerIdentification front-end, replaces input_feature_gen (speaker_identification.py:372-398):
+ * psf.mfcc(winlen .025, winstep .01, nfft 512) -> delta(.,2) -> delta(delta,2) -> [T,39] ->
+ * zero-pad / truncate to 256 frames.  Clips with lens < 4000 are 'silent': silent[c] = 1 and
+ * feat[c] is all zeros.  feat [n,256,39] f32 (float64 arithmetic inside); silent [n] u8 (nullable).
+ */
+int mmla_si_features(mmla_ctx* ctx, const int16_t* pcm, int64_t n_clips, int64_t clip_stride,
+                     const int32_t* lens, int32_t clip_len, float* feat, uint8_t* silent,
+                     uint32_t flags);
+
+/*
+ * Whole-signal SI features cut into 256-frame windows, replaces the conversation-level MFCC +
+ * deltas + chunking of speaker_identification_post_processing.py:255-269 and
+ * make_feature_experiment (speaker_identification.py:340-353).  pcm [n_samples] int16; window s
+ * holds global frames [256 s, 256 s + 256) (deltas edge-padded at the true sequence ends, zero
+ * rows past the last frame).  n_windows must be ceil(T / 256), T = psf frame count of n_samples.
+ * feat [n_windows, 256, 39] f32.
+ */
+int mmla_si_features_seq(mmla_ctx* ctx, const int16_t* pcm, int64_t n_samples, int64_t n_windows,
+                         float* feat, uint32_t flags);
+
+/* OD-NET predict on float NHWC [n,128,151,3] (values 0..255) -> probs [n,2]
+ * (model.predict, record_on_pc.py:159). */
+int mmla_od_forward(mmla_ctx* ctx, const float* x_nhwc, int64_t n, float* probs, uint32_t flags);
+/* Same on the uint8 image produced by mmla_od_features. */
+int mmla_od_forward_u8(mmla_ctx* ctx, const uint8_t* img, int64_t n, float* probs, uint32_t flags);
+
+/* SI-NET predict on [n,256,39] -> probs [n,K] (SI record_on_pc.py:136;
+ * speaker_identification_post_processing.py:272). */
+int mmla_si_forward(mmla_ctx* ctx, const float* x, int64_t n, float* probs, uint32_t flags);
+
+/* Fused WAV->class pipelines (no PNG, no host round trip): probs [n,K] f32 (nullable),
+ * argmax [n] i32 (nullable; -1 for SI 'silent' clips), silent [n] u8 (SI only, nullable). */
+int mmla_od_pipeline(mmla_ctx* ctx, const int16_t* pcm, int64_t n_clips, int64_t clip_stride,
+                     const int32_t* lens, int32_t clip_len, float* probs, int32_t* argmax,
+                     uint32_t flags);
+int mmla_si_pipeline(mmla_ctx* ctx, const int16_t* pcm, int64_t n_clips, int64_t clip_stride,
+                     const int32_t* lens, int32_t clip_len, float* probs, int32_t* argmax,
+                     uint8_t* silent, uint32_t flags);
+
+/*
+ * Kernel tracing (replaces the reference's time.time() prints, overlap_detector_run.py:49-104).
+ * When enabled, every kernel launch is bracketed by hipEvents on the context stream and its device
+ * time is accumulated per stage together with the stage's algorithmic work (bytes for the
+ * front-ends, FLOPs for the networks).  mmla_profile_read waits for the recorded events.
+ */
+#define MMLA_NSTAGES 6
+enum mmla_stage {
+  MMLA_STAGE_OD_FE = 0, /* work = algorithmic HBM bytes */
+  MMLA_STAGE_SI_FE = 1, /* work = algorithmic HBM bytes */
+  MMLA_STAGE_CONV = 2,  /* work = FLOPs (2 * MACs, unpadded) */
+  MMLA_STAGE_LSTM = 3,  /* work = FLOPs */
+  MMLA_STAGE_GLUE = 4,  /* stem, pooling, mean: work = FLOPs */
+  MMLA_STAGE_HEAD = 5   /* dense + softmax / sigmoid: work = FLOPs */
+};
+int mmla_profile_enable(mmla_ctx* ctx, int on);
+/* ms[MMLA_NSTAGES], launches[MMLA_NSTAGES], work[MMLA_NSTAGES] (each nullable); reset != 0 clears */
+int mmla_profile_read(mmla_ctx* ctx, double* ms, int64_t* launches, double* work, int reset);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MMLA_H_ */

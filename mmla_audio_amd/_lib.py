@@ -1,0 +1,293 @@
+"""ctypes binding of libmmla.so (include/mmla.h).  The only way the Python side reaches the GPU.
+
+There is deliberately no CPU fallback: if the in-tree ``libmmla.so`` is missing or no HIP device is
+present, every entry point raises.  (The numpy restatement in ``oracle/`` is test infrastructure and
+is never imported from here.)
+"""
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, 'libmmla.so')
+
+MMLA_OK = 0
+MMLA_DEVICE_PTR = 0x1
+MODEL_OD, MODEL_SI = 0, 1
+HEAD_SOFTMAX, HEAD_SIGMOID = 0, 1
+
+OD_MELS, OD_FRAMES, OD_CLIP = 128, 151, 24000
+SI_FRAMES, SI_DIMS, SI_SILENT_LEN = 256, 39, 4000
+
+_ERRORS = {-1: 'MMLA_E_INVALID', -2: 'MMLA_E_HIP', -3: 'MMLA_E_NOWEIGHTS', -4: 'MMLA_E_OOM',
+           -5: 'MMLA_E_SHAPE'}
+
+_P = ctypes.c_void_p
+_I64 = ctypes.c_int64
+_I32 = ctypes.c_int32
+_U32 = ctypes.c_uint32
+
+# name -> argtypes (all return int)
+SIGNATURES = {
+    'mmla_abi_version': [],
+    'mmla_create': [ctypes.c_int, ctypes.POINTER(_P)],
+    'mmla_destroy': [_P],
+    'mmla_set_stream': [_P, _P],
+    'mmla_synchronize': [_P],
+    'mmla_set_microbatch': [_P, _I64, _I64],
+    'mmla_load_weights': [_P, ctypes.c_int, _P, _I64, _I32, _I32],
+    'mmla_od_features': [_P, _P, _I64, _I64, _P, _I32, _P, _P, _P, _P, _U32],
+    'mmla_si_features': [_P, _P, _I64, _I64, _P, _I32, _P, _P, _U32],
+    'mmla_si_features_seq': [_P, _P, _I64, _I64, _P, _U32],
+    'mmla_od_forward': [_P, _P, _I64, _P, _U32],
+    'mmla_od_forward_u8': [_P, _P, _I64, _P, _U32],
+    'mmla_si_forward': [_P, _P, _I64, _P, _U32],
+    'mmla_od_pipeline': [_P, _P, _I64, _I64, _P, _I32, _P, _P, _U32],
+    'mmla_si_pipeline': [_P, _P, _I64, _I64, _P, _I32, _P, _P, _P, _U32],
+    'mmla_profile_enable': [_P, ctypes.c_int],
+    'mmla_profile_read': [_P, _P, _P, _P, ctypes.c_int],
+}
+
+NSTAGES = 6
+STAGES = ('od_fe', 'si_fe', 'conv', 'lstm', 'glue', 'head')
+
+_lib = None
+_lock = threading.Lock()
+
+
+def load_library(path=LIB_PATH):
+    """dlopen libmmla.so (raises OSError with a build hint if it is absent)."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(path):
+            raise OSError(f'{path} not found: build it with `make -C {os.path.join(_HERE, "csrc")}` '
+                          f'or `python -c "import __graft_entry__ as g; g.build()"`')
+        lib = ctypes.CDLL(path)
+        for name, args in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.argtypes = args
+            fn.restype = ctypes.c_int
+        lib.mmla_last_error.argtypes = [_P]
+        lib.mmla_last_error.restype = ctypes.c_char_p
+        _lib = lib
+        return lib
+
+
+def _ptr(a):
+    if a is None:
+        return None
+    if isinstance(a, int):
+        return a
+    return a.ctypes.data
+
+
+class MmlaError(RuntimeError):
+    pass
+
+
+class Context:
+    """One libmmla context = one HIP device + stream + workspaces + loaded weights.
+
+    Host-array methods take/return numpy arrays (synchronous).  ``*_dev`` methods take raw device
+    pointers (ints, e.g. ``torch_tensor.data_ptr()``) and only enqueue on the context stream.
+    """
+
+    def __init__(self, device=0):
+        self.lib = load_library()
+        h = _P()
+        rc = self.lib.mmla_create(int(device), ctypes.byref(h))
+        if rc != MMLA_OK:
+            raise MmlaError(f'mmla_create(device={device}) failed: {_ERRORS.get(rc, rc)} '
+                            '(no HIP device visible?)')
+        self.h = h
+        self.device = device
+        self.od_classes = None
+        self.si_classes = None
+
+    def close(self):
+        if getattr(self, 'h', None):
+            self.lib.mmla_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc, what):
+        if rc != MMLA_OK:
+            msg = self.lib.mmla_last_error(self.h)
+            raise MmlaError(f'{what}: {_ERRORS.get(rc, rc)}: {msg.decode() if msg else ""}')
+
+    # -- configuration ------------------------------------------------------------------------
+    def set_stream(self, stream_handle):
+        self._check(self.lib.mmla_set_stream(self.h, stream_handle), 'mmla_set_stream')
+
+    def synchronize(self):
+        self._check(self.lib.mmla_synchronize(self.h), 'mmla_synchronize')
+
+    def set_microbatch(self, od=0, si=0):
+        self._check(self.lib.mmla_set_microbatch(self.h, int(od), int(si)), 'mmla_set_microbatch')
+
+    def profile_enable(self, on=True):
+        self._check(self.lib.mmla_profile_enable(self.h, int(bool(on))), 'mmla_profile_enable')
+
+    def profile_read(self, reset=True):
+        """-> {stage: (device ms, launches, algorithmic work)} accumulated since the last reset."""
+        ms = np.zeros(NSTAGES, np.float64)
+        n = np.zeros(NSTAGES, np.int64)
+        wk = np.zeros(NSTAGES, np.float64)
+        self._check(self.lib.mmla_profile_read(self.h, _ptr(ms), _ptr(n), _ptr(wk), int(reset)),
+                    'mmla_profile_read')
+        return {s: (float(ms[i]), int(n[i]), float(wk[i])) for i, s in enumerate(STAGES)}
+
+    def load_weights(self, kind, packed, n_classes, head=HEAD_SOFTMAX):
+        packed = np.ascontiguousarray(packed, dtype=np.float32)
+        self._check(self.lib.mmla_load_weights(self.h, int(kind), _ptr(packed), packed.size,
+                                               int(n_classes), int(head)), 'mmla_load_weights')
+        if kind == MODEL_OD:
+            self.od_classes = int(n_classes)
+        else:
+            self.si_classes = int(n_classes)
+
+    # -- host-array API -----------------------------------------------------------------------
+    @staticmethod
+    def _pcm(pcm, lens):
+        """-> (contiguous int16 [n, L], lens int32 [n] or None, clip_len)."""
+        if isinstance(pcm, (list, tuple)):
+            n = len(pcm)
+            L = max([len(p) for p in pcm] + [1])
+            buf = np.zeros((n, L), np.int16)
+            ln = np.zeros(n, np.int32)
+            for i, p in enumerate(pcm):
+                buf[i, :len(p)] = np.asarray(p, np.int16)
+                ln[i] = len(p)
+            return buf, ln, L
+        a = np.ascontiguousarray(pcm, dtype=np.int16)
+        if a.ndim == 1:
+            a = a[None]
+        ln = None if lens is None else np.ascontiguousarray(lens, dtype=np.int32)
+        return a, ln, a.shape[1]
+
+    def od_features(self, pcm, lens=None, db=True, norm=True, zcr=True, img=True):
+        a, ln, L = self._pcm(pcm, lens)
+        n = a.shape[0]
+        out = {}
+        bufs = {}
+        for key, want, shape, dt in (('db', db, (n, OD_MELS, OD_FRAMES), np.float32),
+                                     ('norm', norm, (n, OD_MELS, OD_FRAMES), np.float32),
+                                     ('zcr', zcr, (n, OD_FRAMES), np.float32),
+                                     ('img', img, (n, OD_MELS, OD_FRAMES, 3), np.uint8)):
+            bufs[key] = np.empty(shape, dt) if want else None
+        self._check(self.lib.mmla_od_features(
+            self.h, _ptr(a), n, a.shape[1], _ptr(ln), L, _ptr(bufs['db']), _ptr(bufs['norm']),
+            _ptr(bufs['zcr']), _ptr(bufs['img']), 0), 'mmla_od_features')
+        for k, v in bufs.items():
+            if v is not None:
+                out[k] = v
+        return out
+
+    def si_features(self, pcm, lens=None):
+        a, ln, L = self._pcm(pcm, lens)
+        n = a.shape[0]
+        feat = np.empty((n, SI_FRAMES, SI_DIMS), np.float32)
+        silent = np.empty(n, np.uint8)
+        self._check(self.lib.mmla_si_features(self.h, _ptr(a), n, a.shape[1], _ptr(ln), L,
+                                              _ptr(feat), _ptr(silent), 0), 'mmla_si_features')
+        return feat, silent.astype(bool)
+
+    def si_features_seq(self, sig):
+        """Whole-signal features cut into 256-frame windows -> float32 [S, 256, 39]."""
+        sig = np.ascontiguousarray(sig, dtype=np.int16).ravel()
+        n = sig.size
+        T = 1 if n <= 400 else 1 + -(-(n - 400) // 160)
+        S = -(-T // SI_FRAMES)
+        feat = np.empty((S, SI_FRAMES, SI_DIMS), np.float32)
+        self._check(self.lib.mmla_si_features_seq(self.h, _ptr(sig), n, S, _ptr(feat), 0),
+                    'mmla_si_features_seq')
+        return feat
+
+    def od_forward(self, x):
+        x = np.ascontiguousarray(x)
+        n = x.shape[0]
+        probs = np.empty((n, 2), np.float32)
+        if x.dtype == np.uint8:
+            rc = self.lib.mmla_od_forward_u8(self.h, _ptr(x), n, _ptr(probs), 0)
+        else:
+            x = np.ascontiguousarray(x, dtype=np.float32)
+            rc = self.lib.mmla_od_forward(self.h, _ptr(x), n, _ptr(probs), 0)
+        self._check(rc, 'mmla_od_forward')
+        return probs
+
+    def si_forward(self, x):
+        x = np.ascontiguousarray(x, dtype=np.float32)
+        n = x.shape[0]
+        probs = np.empty((n, self.si_classes or 0), np.float32)
+        self._check(self.lib.mmla_si_forward(self.h, _ptr(x), n, _ptr(probs), 0), 'mmla_si_forward')
+        return probs
+
+    def od_pipeline(self, pcm, lens=None):
+        a, ln, L = self._pcm(pcm, lens)
+        n = a.shape[0]
+        probs = np.empty((n, 2), np.float32)
+        am = np.empty(n, np.int32)
+        self._check(self.lib.mmla_od_pipeline(self.h, _ptr(a), n, a.shape[1], _ptr(ln), L,
+                                              _ptr(probs), _ptr(am), 0), 'mmla_od_pipeline')
+        return probs, am
+
+    def si_pipeline(self, pcm, lens=None):
+        a, ln, L = self._pcm(pcm, lens)
+        n = a.shape[0]
+        probs = np.empty((n, self.si_classes or 0), np.float32)
+        am = np.empty(n, np.int32)
+        silent = np.empty(n, np.uint8)
+        self._check(self.lib.mmla_si_pipeline(self.h, _ptr(a), n, a.shape[1], _ptr(ln), L,
+                                              _ptr(probs), _ptr(am), _ptr(silent), 0),
+                    'mmla_si_pipeline')
+        return probs, am, silent.astype(bool)
+
+    # -- device-pointer API (asynchronous on the context stream) -------------------------------
+    def od_features_dev(self, pcm, n, stride, clip_len, db=0, norm=0, zcr=0, img=0, lens=0):
+        self._check(self.lib.mmla_od_features(self.h, pcm, n, stride, lens or None, clip_len,
+                                              db or None, norm or None, zcr or None, img or None,
+                                              MMLA_DEVICE_PTR), 'mmla_od_features(dev)')
+
+    def si_features_dev(self, pcm, n, stride, clip_len, feat, silent=0, lens=0):
+        self._check(self.lib.mmla_si_features(self.h, pcm, n, stride, lens or None, clip_len, feat,
+                                              silent or None, MMLA_DEVICE_PTR),
+                    'mmla_si_features(dev)')
+
+    def od_pipeline_dev(self, pcm, n, stride, clip_len, probs=0, argmax=0, lens=0):
+        self._check(self.lib.mmla_od_pipeline(self.h, pcm, n, stride, lens or None, clip_len,
+                                              probs or None, argmax or None, MMLA_DEVICE_PTR),
+                    'mmla_od_pipeline(dev)')
+
+    def si_pipeline_dev(self, pcm, n, stride, clip_len, probs=0, argmax=0, silent=0, lens=0):
+        self._check(self.lib.mmla_si_pipeline(self.h, pcm, n, stride, lens or None, clip_len,
+                                              probs or None, argmax or None, silent or None,
+                                              MMLA_DEVICE_PTR), 'mmla_si_pipeline(dev)')
+
+    def od_forward_dev(self, x, n, probs, u8=False):
+        fn = self.lib.mmla_od_forward_u8 if u8 else self.lib.mmla_od_forward
+        self._check(fn(self.h, x, n, probs, MMLA_DEVICE_PTR), 'mmla_od_forward(dev)')
+
+    def si_forward_dev(self, x, n, probs):
+        self._check(self.lib.mmla_si_forward(self.h, x, n, probs, MMLA_DEVICE_PTR),
+                    'mmla_si_forward(dev)')
+
+
+_default = {}
+
+
+def default_context(device=None):
+    """Process-wide context per device (device defaults to LOCAL_RANK or 0)."""
+    if device is None:
+        device = int(os.environ.get('LOCAL_RANK', 0))
+    if device not in _default:
+        _default[device] = Context(device)
+    return _default[device]

@@ -1,0 +1,920 @@
+// libmmla C ABI: context, weights, and the OD / SI pipelines over the HIP kernels.
+// See include/mmla.h for the contract and the reference call site each entry point replaces.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/mmla.h"
+#include "conv.h"
+#include "nets.h"
+#include "od_fe.h"
+#include "si_fe.h"
+
+namespace {
+
+constexpr int OD_H = 128, OD_W = 151, OD_PIX = OD_H * OD_W;
+constexpr int OD_IMG = OD_PIX * 3;
+constexpr int SI_T = 256, SI_D = 39;
+constexpr int SI_NEED_SAMPLES = 160 * 259 + 400;   // frames 0..259 (delta-delta reach)
+constexpr int CH[9] = {32, 32, 32, 64, 64, 64, 128, 128, 128};
+constexpr bool POOL[9] = {true, false, false, true, false, false, true, false, false};
+
+struct ConvW {
+  float* wt = nullptr;
+  float* bias = nullptr;
+  int kh = 0, kw = 0, cin = 0, cout = 0, cout_pad = 0;
+};
+struct BnW {
+  float* scale = nullptr;
+  float* shift = nullptr;
+  int c = 0;
+};
+struct LstmW {
+  float* wcat[2] = {nullptr, nullptr};
+  float* bias[2] = {nullptr, nullptr};
+};
+struct OdBlock {
+  BnW bn_in, bn_mid;
+  ConvW c3, c4, sc;
+};
+struct SiUnit {
+  BnW bn_in, bn_mid;
+  ConvW ca, cb, sc;
+};
+struct OdNet {
+  ConvW stem;
+  OdBlock blk[9];
+  LstmW lstm;
+  float* head_w = nullptr;
+  float* head_b = nullptr;
+};
+struct SiNet {
+  ConvW stem;
+  SiUnit unit[9];
+  BnW final_bn;
+  LstmW lstm;
+  ConvW dense;
+  int k = 0, head = 0;
+};
+
+struct ProfRec {
+  int stage;
+  hipEvent_t a, b;
+  double work;
+};
+
+}  // namespace
+
+struct mmla_ctx {
+  bool prof_on = false;
+  std::vector<ProfRec> prof_pending;
+  std::vector<hipEvent_t> prof_pool;
+  double prof_ms[MMLA_NSTAGES] = {0};
+  double prof_work[MMLA_NSTAGES] = {0};
+  int64_t prof_n[MMLA_NSTAGES] = {0};
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipStream_t own_stream = nullptr;
+  std::string err;
+  OdFeTables* od_tables = nullptr;
+  SiFeTables* si_tables = nullptr;
+  bool od_loaded = false, si_loaded = false;
+  OdNet od;
+  SiNet si;
+  std::vector<void*> od_allocs, si_allocs;
+  std::vector<void*> ws;
+  std::vector<size_t> ws_size;
+  int64_t od_mb = 4096, si_mb = 16384;
+};
+
+namespace {
+
+int fail(mmla_ctx* c, int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  if (c) c->err = buf;
+  return code;
+}
+
+#define HIPCHK(ctx, expr)                                                                    \
+  do {                                                                                       \
+    hipError_t e_ = (expr);                                                                  \
+    if (e_ != hipSuccess)                                                                    \
+      return fail(ctx, MMLA_E_HIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_),   \
+                  __FILE__, __LINE__);                                                       \
+  } while (0)
+
+#define CHK(expr)              \
+  do {                         \
+    int r_ = (expr);           \
+    if (r_ != MMLA_OK) return r_; \
+  } while (0)
+
+// ---- tracing: hipEvents around each launch when enabled ---------------------------------------
+hipEvent_t prof_event(mmla_ctx* c) {
+  if (!c->prof_pool.empty()) {
+    hipEvent_t e = c->prof_pool.back();
+    c->prof_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  (void)hipEventCreate(&e);
+  return e;
+}
+
+int prof_begin(mmla_ctx* c, int stage) {
+  if (!c->prof_on) return -1;
+  ProfRec r{stage, prof_event(c), prof_event(c), 0.0};
+  (void)hipEventRecord(r.a, c->stream);
+  c->prof_pending.push_back(r);
+  return (int)c->prof_pending.size() - 1;
+}
+
+void prof_end(mmla_ctx* c, int idx, double work) {
+  if (idx < 0) return;
+  ProfRec& r = c->prof_pending[idx];
+  r.work = work;
+  (void)hipEventRecord(r.b, c->stream);
+}
+
+int prof_collect(mmla_ctx* c) {
+  for (ProfRec& r : c->prof_pending) {
+    HIPCHK(c, hipEventSynchronize(r.b));
+    float ms = 0.0f;
+    HIPCHK(c, hipEventElapsedTime(&ms, r.a, r.b));
+    c->prof_ms[r.stage] += ms;
+    c->prof_work[r.stage] += r.work;
+    c->prof_n[r.stage] += 1;
+    c->prof_pool.push_back(r.a);
+    c->prof_pool.push_back(r.b);
+  }
+  c->prof_pending.clear();
+  return MMLA_OK;
+}
+
+// launch `expr` (a hipError_t-returning launcher) as stage `st` with algorithmic work `wk`
+#define LAUNCH(c, st, wk, expr)            \
+  do {                                     \
+    const int pi_ = prof_begin((c), (st)); \
+    HIPCHK((c), (expr));                   \
+    prof_end((c), pi_, (wk));              \
+  } while (0)
+
+// growable device workspace slots
+int ws_get(mmla_ctx* c, int slot, size_t bytes, void** out) {
+  if ((int)c->ws.size() <= slot) {
+    c->ws.resize(slot + 1, nullptr);
+    c->ws_size.resize(slot + 1, 0);
+  }
+  if (c->ws_size[slot] < bytes) {
+    if (c->ws[slot]) {
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      HIPCHK(c, hipFree(c->ws[slot]));
+      c->ws[slot] = nullptr;
+      c->ws_size[slot] = 0;
+    }
+    void* p = nullptr;
+    if (hipMalloc(&p, bytes) != hipSuccess)
+      return fail(c, MMLA_E_OOM, "hipMalloc(%zu) failed for workspace slot %d", bytes, slot);
+    c->ws[slot] = p;
+    c->ws_size[slot] = bytes;
+  }
+  *out = c->ws[slot];
+  return MMLA_OK;
+}
+
+enum Slot {
+  S_PCM = 0, S_LENS, S_IMG, S_X, S_T1, S_T2, S_T3, S_SEQ, S_HOUT, S_LOGIT, S_FEAT, S_SILENT,
+  S_OUT0, S_OUT1, S_OUT2, S_OUT3, S_IN
+};
+
+// ---- weights -------------------------------------------------------------------------------------
+
+struct Cursor {
+  const float* p;
+  int64_t left;
+  bool ok = true;
+  const float* take(int64_t n) {
+    if (n > left) {
+      ok = false;
+      return nullptr;
+    }
+    const float* r = p;
+    p += n;
+    left -= n;
+    return r;
+  }
+};
+
+int upload(mmla_ctx* c, std::vector<void*>& allocs, const void* host, size_t bytes, float** out) {
+  void* d = nullptr;
+  if (hipMalloc(&d, bytes) != hipSuccess) return fail(c, MMLA_E_OOM, "weight hipMalloc failed");
+  allocs.push_back(d);
+  HIPCHK(c, hipMemcpy(d, host, bytes, hipMemcpyHostToDevice));
+  *out = static_cast<float*>(d);
+  return MMLA_OK;
+}
+
+int take_conv(mmla_ctx* c, Cursor& cur, std::vector<void*>& al, int kh, int kw, int cin, int cout,
+              ConvW* w) {
+  const float* k = cur.take((int64_t)kh * kw * cin * cout);
+  const float* b = cur.take(cout);
+  if (!cur.ok) return fail(c, MMLA_E_SHAPE, "weight blob too short");
+  w->kh = kh;
+  w->kw = kw;
+  w->cin = cin;
+  w->cout = cout;
+  w->cout_pad = (cout + 31) / 32 * 32;
+  if (w->cout_pad > 128) w->cout_pad = (cout + 127) / 128 * 128;
+  std::vector<float> kp((size_t)kh * kw * cin * w->cout_pad, 0.0f), bp(w->cout_pad, 0.0f);
+  for (int64_t r = 0; r < (int64_t)kh * kw * cin; ++r)
+    memcpy(&kp[r * w->cout_pad], k + r * cout, sizeof(float) * cout);
+  memcpy(bp.data(), b, sizeof(float) * cout);
+  CHK(upload(c, al, kp.data(), kp.size() * sizeof(float), &w->wt));
+  CHK(upload(c, al, bp.data(), bp.size() * sizeof(float), &w->bias));
+  return MMLA_OK;
+}
+
+int take_bn(mmla_ctx* c, Cursor& cur, std::vector<void*>& al, int ch, BnW* bn) {
+  const float* g = cur.take(ch);
+  const float* be = cur.take(ch);
+  const float* m = cur.take(ch);
+  const float* v = cur.take(ch);
+  if (!cur.ok) return fail(c, MMLA_E_SHAPE, "weight blob too short");
+  std::vector<float> sc(ch), sh(ch);
+  for (int i = 0; i < ch; ++i) {   // Keras BN(eps=1e-3) inference: x * s + (beta - mean * s)
+    const double s = (double)g[i] / std::sqrt((double)v[i] + 1e-3);
+    sc[i] = (float)s;
+    sh[i] = (float)((double)be[i] - (double)m[i] * s);
+  }
+  bn->c = ch;
+  CHK(upload(c, al, sc.data(), ch * sizeof(float), &bn->scale));
+  CHK(upload(c, al, sh.data(), ch * sizeof(float), &bn->shift));
+  return MMLA_OK;
+}
+
+int take_lstm(mmla_ctx* c, Cursor& cur, std::vector<void*>& al, int d, LstmW* l) {
+  for (int dir = 0; dir < 2; ++dir) {
+    const float* k = cur.take((int64_t)d * 1024);
+    const float* r = cur.take(256 * 1024);
+    const float* b = cur.take(1024);
+    if (!cur.ok) return fail(c, MMLA_E_SHAPE, "weight blob too short");
+    std::vector<float> wc((size_t)(256 + d) * 1024);
+    memcpy(wc.data(), r, sizeof(float) * 256 * 1024);
+    memcpy(wc.data() + 256 * 1024, k, sizeof(float) * d * 1024);
+    CHK(upload(c, al, wc.data(), wc.size() * sizeof(float), &l->wcat[dir]));
+    CHK(upload(c, al, b, 1024 * sizeof(float), &l->bias[dir]));
+  }
+  return MMLA_OK;
+}
+
+void free_allocs(std::vector<void*>& al) {
+  for (void* p : al) (void)hipFree(p);
+  al.clear();
+}
+
+// ---- PCM staging -------------------------------------------------------------------------------
+
+struct Pcm {
+  const int16_t* p;
+  int64_t stride;
+  const int32_t* lens;
+  int32_t clip_len;
+};
+
+// Device view of clips [c0, c0 + cnt): offsets in device mode, a dense copy of the first
+// `need` samples per clip in host mode.
+int stage_pcm(mmla_ctx* c, const int16_t* pcm, int64_t c0, int64_t cnt, int64_t stride,
+              const int32_t* lens, int32_t clip_len, int need, bool dev, Pcm* out) {
+  if (dev) {
+    *out = {pcm + c0 * stride, stride, lens ? lens + c0 : nullptr, clip_len};
+    return MMLA_OK;
+  }
+  int64_t width = lens ? std::min<int64_t>(need, stride) : std::min<int64_t>(need, clip_len);
+  if (width < 1) width = 1;
+  void* dp = nullptr;
+  CHK(ws_get(c, S_PCM, (size_t)cnt * width * sizeof(int16_t), &dp));
+  HIPCHK(c, hipMemcpy2DAsync(dp, width * sizeof(int16_t), pcm + c0 * stride, stride * sizeof(int16_t),
+                             width * sizeof(int16_t), cnt, hipMemcpyHostToDevice, c->stream));
+  int32_t* dl = nullptr;
+  if (lens) {
+    void* lp = nullptr;
+    CHK(ws_get(c, S_LENS, (size_t)cnt * sizeof(int32_t), &lp));
+    HIPCHK(c, hipMemcpyAsync(lp, lens + c0, cnt * sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
+    dl = static_cast<int32_t*>(lp);
+  }
+  *out = {static_cast<int16_t*>(dp), width, dl, (int32_t)std::min<int64_t>(clip_len, width)};
+  return MMLA_OK;
+}
+
+// device destination for an output chunk: the caller's pointer (device mode) or a staging slot
+template <typename T>
+int out_ptr(mmla_ctx* c, T* user, int64_t off, size_t count, bool dev, int slot, T** d) {
+  if (!user) {
+    *d = nullptr;
+    return MMLA_OK;
+  }
+  if (dev) {
+    *d = user + off;
+    return MMLA_OK;
+  }
+  void* p = nullptr;
+  CHK(ws_get(c, slot, count * sizeof(T), &p));
+  *d = static_cast<T*>(p);
+  return MMLA_OK;
+}
+
+template <typename T>
+int copy_back(mmla_ctx* c, T* user, int64_t off, const T* d, size_t count, bool dev) {
+  if (!user || dev) return MMLA_OK;
+  HIPCHK(c, hipMemcpyAsync(user + off, d, count * sizeof(T), hipMemcpyDeviceToHost, c->stream));
+  return MMLA_OK;
+}
+
+int finish(mmla_ctx* c, bool dev) {
+  HIPCHK(c, hipGetLastError());
+  if (!dev) HIPCHK(c, hipStreamSynchronize(c->stream));
+  return MMLA_OK;
+}
+
+// ---- network runners (device pointers, one micro-batch) -----------------------------------------
+
+ConvArgs conv_args(const ConvW& w, const float* x, float* y, int n, int h, int wd, int stride,
+                   const BnW* bn, int pro, int epi, const float* res) {
+  ConvArgs a{};
+  a.x = x;
+  a.wt = w.wt;
+  a.bias = w.bias;
+  a.scale = bn ? bn->scale : nullptr;
+  a.shift = bn ? bn->shift : nullptr;
+  a.res = res;
+  a.y = y;
+  a.n = n;
+  a.h = h;
+  a.w = wd;
+  a.cin = w.cin;
+  a.ho = (h + stride - 1) / stride;
+  a.wo = (wd + stride - 1) / stride;
+  a.cout = w.cout;
+  a.cout_pad = w.cout_pad;
+  a.ldy = w.cout;
+  a.kh = w.kh;
+  a.kw = w.kw;
+  a.stride = stride;
+  const int th = std::max((a.ho - 1) * stride + w.kh - h, 0);
+  const int tw = std::max((a.wo - 1) * stride + w.kw - wd, 0);
+  a.pad_h = th / 2;   // Keras 'same': extra padding goes after
+  a.pad_w = tw / 2;
+  a.pro = pro;
+  a.epi = epi;
+  return a;
+}
+
+double conv_flops(const ConvArgs& a) {
+  return 2.0 * (double)a.n * a.ho * a.wo * a.kh * a.kw * a.cin * a.cout;
+}
+
+int conv_run(mmla_ctx* c, const ConvArgs& a, int stage = MMLA_STAGE_CONV) {
+  LAUNCH(c, stage, conv_flops(a), conv_launch(a, c->stream));
+  return MMLA_OK;
+}
+
+double lstm_flops(int64_t n, int T, int D) { return 2.0 * n * T * 2 * (256.0 + D) * 1024.0; }
+
+// OD-NET on a device batch; input = uint8 image (img_u8) or float NHWC (img_f32).
+int run_od_net(mmla_ctx* c, const uint8_t* img_u8, const float* img_f32, int64_t n, float* probs,
+               int32_t* argmax) {
+  const OdNet& W = c->od;
+  const size_t big = (size_t)n * OD_PIX * 32 * sizeof(float);
+  void *px, *pt1, *pt2, *pseq, *ph;
+  CHK(ws_get(c, S_X, big, &px));
+  CHK(ws_get(c, S_T1, big, &pt1));
+  CHK(ws_get(c, S_T2, big, &pt2));
+  CHK(ws_get(c, S_SEQ, (size_t)n * 19 * 128 * sizeof(float), &pseq));
+  CHK(ws_get(c, S_HOUT, (size_t)n * 512 * sizeof(float), &ph));
+  float* X = static_cast<float*>(px);
+  float* T1 = static_cast<float*>(pt1);
+  float* T2 = static_cast<float*>(pt2);
+  // Conv2D(16, 1x1) on the PNG image (overlap_detector_temp.py:282)
+  LAUNCH(c, MMLA_STAGE_GLUE, 2.0 * n * OD_PIX * 3 * 16,
+         od_stem_launch(img_u8, img_f32, n * OD_PIX, W.stem.wt, W.stem.bias, X, c->stream));
+  int h = OD_H, w = OD_W;
+  for (int b = 0; b < 9; ++b) {   // res_block, overlap_detector_temp.py:253-277
+    const OdBlock& B = W.blk[b];
+    CHK(conv_run(c, conv_args(B.c3, X, T1, (int)n, h, w, 1, &B.bn_in, PRO_BN_ELU, EPI_BIAS, nullptr)));
+    if (POOL[b]) {
+      CHK(conv_run(c, conv_args(B.c4, T1, T2, (int)n, h, w, 1, &B.bn_mid, PRO_BN_ELU, EPI_BIAS,
+                                nullptr)));
+      // shortcut Conv2D(1x1, stride 2) + MaxPool2D(2, 'same')(t2), fused
+      ConvArgs s = conv_args(B.sc, X, T1, (int)n, h, w, 2, nullptr, PRO_NONE, EPI_ADD_POOL, T2);
+      s.hp = h;
+      s.wp = w;
+      CHK(conv_run(c, s));
+      std::swap(X, T1);
+      h = (h + 1) / 2;
+      w = (w + 1) / 2;
+    } else {
+      CHK(conv_run(c, conv_args(B.c4, T1, X, (int)n, h, w, 1, &B.bn_mid, PRO_BN_ELU, EPI_ADD, X)));
+    }
+  }
+  // h = 16, w = 19, c = 128: Lambda(K.mean(x, axis=1)) -> [n, 19, 128]
+  LAUNCH(c, MMLA_STAGE_GLUE, (double)n * h * w * 128,
+         mean_h_launch(X, (int)n, h, w, 128, static_cast<float*>(pseq), c->stream));
+  LAUNCH(c, MMLA_STAGE_LSTM, lstm_flops(n, w, 128),
+         bilstm_launch(static_cast<float*>(pseq), (int)n, w, 128, W.lstm.wcat[0], W.lstm.wcat[1],
+                       W.lstm.bias[0], W.lstm.bias[1], static_cast<float*>(ph), c->stream));
+  LAUNCH(c, MMLA_STAGE_HEAD, 2.0 * n * 512 * 2,
+         od_head_launch(static_cast<float*>(ph), (int)n, W.head_w, W.head_b, probs, argmax,
+                        c->stream));
+  return MMLA_OK;
+}
+
+int run_si_net(mmla_ctx* c, const float* x, int64_t n, float* probs, int32_t* argmax,
+               const uint8_t* silent) {
+  const SiNet& W = c->si;
+  const size_t big = (size_t)n * SI_T * 32 * sizeof(float);
+  void *px, *pt1, *pt2, *pt3, *pseq, *ph, *pl;
+  CHK(ws_get(c, S_X, big, &px));
+  CHK(ws_get(c, S_T1, big, &pt1));
+  CHK(ws_get(c, S_T2, big, &pt2));
+  CHK(ws_get(c, S_T3, big, &pt3));
+  CHK(ws_get(c, S_SEQ, (size_t)n * 8 * 128 * sizeof(float), &pseq));
+  CHK(ws_get(c, S_HOUT, (size_t)n * 512 * sizeof(float), &ph));
+  CHK(ws_get(c, S_LOGIT, (size_t)n * W.dense.cout_pad * sizeof(float), &pl));
+  float* X = static_cast<float*>(px);
+  float* T1 = static_cast<float*>(pt1);
+  float* XP = static_cast<float*>(pt2);
+  float* R = static_cast<float*>(pt3);
+  int t = SI_T;
+  // Conv1D(32, 4, same): [n, 256, 1, 39] -> [n, 256, 1, 32] (speaker_identification.py:195)
+  CHK(conv_run(c, conv_args(W.stem, x, X, (int)n, t, 1, 1, nullptr, PRO_NONE, EPI_BIAS, nullptr)));
+  for (int u = 0; u < 9; ++u) {   // res_unit, speaker_identification.py:168-190
+    const SiUnit& U = W.unit[u];
+    const int cin = U.ca.cin;
+    if (POOL[u]) {
+      LAUNCH(c, MMLA_STAGE_GLUE, (double)n * t * cin,
+             maxpool_t2_launch(X, (int)n, t, cin, XP, c->stream));
+      const int tp = (t + 1) / 2;
+      CHK(conv_run(c, conv_args(U.ca, XP, T1, (int)n, tp, 1, 1, &U.bn_in, PRO_BN_RELU, EPI_BIAS,
+                                nullptr)));
+      CHK(conv_run(c, conv_args(U.sc, X, R, (int)n, t, 1, 2, nullptr, PRO_NONE, EPI_BIAS, nullptr)));
+      CHK(conv_run(c, conv_args(U.cb, T1, R, (int)n, tp, 1, 1, &U.bn_mid, PRO_BN_RELU, EPI_ADD, R)));
+      std::swap(X, R);
+      t = tp;
+    } else {
+      CHK(conv_run(c, conv_args(U.ca, X, T1, (int)n, t, 1, 1, &U.bn_in, PRO_BN_RELU, EPI_BIAS,
+                                nullptr)));
+      CHK(conv_run(c, conv_args(U.cb, T1, X, (int)n, t, 1, 1, &U.bn_mid, PRO_BN_RELU, EPI_ADD, X)));
+    }
+  }
+  // t = 32, c = 128 -> BN -> ReLU -> AvgPool1D(4) -> [n, 8, 128] (speaker_identification.py:208-212)
+  LAUNCH(c, MMLA_STAGE_GLUE, 3.0 * n * t * 128,
+         bn_relu_avgpool4_launch(X, (int)n, t, 128, W.final_bn.scale, W.final_bn.shift,
+                                 static_cast<float*>(pseq), c->stream));
+  LAUNCH(c, MMLA_STAGE_LSTM, lstm_flops(n, t / 4, 128),
+         bilstm_launch(static_cast<float*>(pseq), (int)n, t / 4, 128, W.lstm.wcat[0],
+                       W.lstm.wcat[1], W.lstm.bias[0], W.lstm.bias[1], static_cast<float*>(ph),
+                       c->stream));
+  ConvArgs d = conv_args(W.dense, static_cast<float*>(ph), static_cast<float*>(pl), (int)n, 1, 1, 1,
+                         nullptr, PRO_NONE, EPI_BIAS, nullptr);
+  d.ldy = W.dense.cout_pad;
+  CHK(conv_run(c, d, MMLA_STAGE_HEAD));
+  LAUNCH(c, MMLA_STAGE_HEAD, 4.0 * n * W.k,
+         si_head_launch(static_cast<float*>(pl), (int)n, W.k, W.dense.cout_pad, W.head, probs,
+                        argmax, silent, c->stream));
+  return MMLA_OK;
+}
+
+// algorithmic HBM bytes of one front-end launch: PCM actually consumed + outputs
+double od_fe_bytes(int64_t n, const OdFeArgs& a) {
+  const double in = a.lens ? (double)MMLA_OD_CLIP * 2 : (double)std::min(a.clip_len, MMLA_OD_CLIP) * 2;
+  const double out = (a.db ? OD_PIX * 4.0 : 0) + (a.norm ? OD_PIX * 4.0 : 0) +
+                     (a.zcr ? OD_W * 4.0 : 0) + (a.img ? (double)OD_IMG : 0);
+  return (double)n * (in + out);
+}
+
+double si_fe_bytes(int64_t n, const SiFeArgs& a) {
+  const double in = a.lens ? (double)SI_NEED_SAMPLES * 2 : (double)std::min(a.clip_len, SI_NEED_SAMPLES) * 2;
+  return (double)n * (in + SI_T * SI_D * 4.0 + (a.silent ? 1.0 : 0.0));
+}
+
+bool bad_pcm_args(const int16_t* pcm, int64_t n, int64_t stride, const int32_t* lens,
+                  int32_t clip_len) {
+  if (n < 0 || (n > 0 && !pcm)) return true;
+  if (!lens && clip_len < 0) return true;
+  if (!lens && n > 1 && stride < clip_len) return true;
+  return false;
+}
+
+}  // namespace
+
+// ==== C ABI =========================================================================================
+
+extern "C" {
+
+int mmla_abi_version(void) { return MMLA_ABI_VERSION; }
+
+int mmla_create(int device, mmla_ctx** out) {
+  if (!out) return MMLA_E_INVALID;
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return MMLA_E_HIP;
+  if (device < 0 || device >= ndev) return MMLA_E_INVALID;
+  if (hipSetDevice(device) != hipSuccess) return MMLA_E_HIP;
+  mmla_ctx* c = new mmla_ctx();
+  c->device = device;
+  if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return MMLA_E_HIP;
+  }
+  c->stream = c->own_stream;
+  OdFeTables ot;
+  od_fe_build_tables(&ot);
+  SiFeTables st;
+  si_fe_build_tables(&st);
+  if (hipMalloc(&c->od_tables, sizeof(OdFeTables)) != hipSuccess ||
+      hipMalloc(&c->si_tables, sizeof(SiFeTables)) != hipSuccess ||
+      hipMemcpy(c->od_tables, &ot, sizeof(ot), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(c->si_tables, &st, sizeof(st), hipMemcpyHostToDevice) != hipSuccess) {
+    mmla_destroy(c);
+    return MMLA_E_HIP;
+  }
+  *out = c;
+  return MMLA_OK;
+}
+
+int mmla_destroy(mmla_ctx* c) {
+  if (!c) return MMLA_E_INVALID;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  free_allocs(c->od_allocs);
+  free_allocs(c->si_allocs);
+  for (void* p : c->ws)
+    if (p) (void)hipFree(p);
+  if (c->od_tables) (void)hipFree(c->od_tables);
+  if (c->si_tables) (void)hipFree(c->si_tables);
+  (void)prof_collect(c);
+  for (hipEvent_t e : c->prof_pool) (void)hipEventDestroy(e);
+  if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+  delete c;
+  return MMLA_OK;
+}
+
+const char* mmla_last_error(const mmla_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int mmla_set_stream(mmla_ctx* c, void* s) {
+  if (!c) return MMLA_E_INVALID;
+  c->stream = s ? static_cast<hipStream_t>(s) : c->own_stream;
+  return MMLA_OK;
+}
+
+int mmla_synchronize(mmla_ctx* c) {
+  if (!c) return MMLA_E_INVALID;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return MMLA_OK;
+}
+
+int mmla_set_microbatch(mmla_ctx* c, int64_t od, int64_t si) {
+  if (!c || od < 0 || si < 0) return MMLA_E_INVALID;
+  if (od) c->od_mb = od;
+  if (si) c->si_mb = si;
+  return MMLA_OK;
+}
+
+int mmla_load_weights(mmla_ctx* c, int kind, const float* packed, int64_t n_floats,
+                      int32_t n_classes, int32_t head) {
+  if (!c) return MMLA_E_INVALID;
+  if (!packed || n_floats <= 0) return fail(c, MMLA_E_INVALID, "null weight blob");
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  Cursor cur{packed, n_floats};
+  if (kind == MMLA_MODEL_OD) {
+    if (n_classes != 2) return fail(c, MMLA_E_INVALID, "OD model has 2 classes, got %d", n_classes);
+    free_allocs(c->od_allocs);
+    c->od_loaded = false;
+    OdNet& W = c->od;
+    auto& al = c->od_allocs;
+    CHK(take_conv(c, cur, al, 1, 1, 3, 16, &W.stem));
+    int cin = 16;
+    for (int b = 0; b < 9; ++b) {
+      const int ch = CH[b];
+      CHK(take_bn(c, cur, al, cin, &W.blk[b].bn_in));
+      CHK(take_conv(c, cur, al, 3, 3, cin, ch, &W.blk[b].c3));
+      CHK(take_bn(c, cur, al, ch, &W.blk[b].bn_mid));
+      CHK(take_conv(c, cur, al, 4, 1, ch, ch, &W.blk[b].c4));
+      if (POOL[b]) CHK(take_conv(c, cur, al, 1, 1, cin, ch, &W.blk[b].sc));
+      cin = ch;
+    }
+    CHK(take_lstm(c, cur, al, 128, &W.lstm));
+    const float* hw = cur.take(512 * 2);
+    const float* hb = cur.take(2);
+    if (!cur.ok) return fail(c, MMLA_E_SHAPE, "OD weight blob too short");
+    CHK(upload(c, al, hw, 512 * 2 * sizeof(float), &W.head_w));
+    CHK(upload(c, al, hb, 2 * sizeof(float), &W.head_b));
+    if (cur.left != 0)
+      return fail(c, MMLA_E_SHAPE, "OD weight blob has %lld extra floats", (long long)cur.left);
+    c->od_loaded = true;
+    return MMLA_OK;
+  }
+  if (kind == MMLA_MODEL_SI) {
+    if (n_classes < 1) return fail(c, MMLA_E_INVALID, "SI n_classes must be >= 1");
+    if (head != MMLA_HEAD_SOFTMAX && head != MMLA_HEAD_SIGMOID)
+      return fail(c, MMLA_E_INVALID, "unknown head %d", head);
+    free_allocs(c->si_allocs);
+    c->si_loaded = false;
+    SiNet& W = c->si;
+    auto& al = c->si_allocs;
+    CHK(take_conv(c, cur, al, 4, 1, 39, 32, &W.stem));
+    int cin = 32;
+    for (int u = 0; u < 9; ++u) {
+      const int ch = CH[u];
+      CHK(take_bn(c, cur, al, cin, &W.unit[u].bn_in));
+      CHK(take_conv(c, cur, al, 3, 1, cin, ch, &W.unit[u].ca));
+      CHK(take_bn(c, cur, al, ch, &W.unit[u].bn_mid));
+      if (POOL[u]) CHK(take_conv(c, cur, al, 1, 1, cin, ch, &W.unit[u].sc));
+      CHK(take_conv(c, cur, al, 3, 1, ch, ch, &W.unit[u].cb));
+      cin = ch;
+    }
+    CHK(take_bn(c, cur, al, 128, &W.final_bn));
+    CHK(take_lstm(c, cur, al, 128, &W.lstm));
+    CHK(take_conv(c, cur, al, 1, 1, 512, n_classes, &W.dense));
+    if (cur.left != 0)
+      return fail(c, MMLA_E_SHAPE, "SI weight blob has %lld extra floats", (long long)cur.left);
+    W.k = n_classes;
+    W.head = head;
+    c->si_loaded = true;
+    return MMLA_OK;
+  }
+  return fail(c, MMLA_E_INVALID, "unknown model kind %d", kind);
+}
+
+int mmla_od_features(mmla_ctx* c, const int16_t* pcm, int64_t n, int64_t stride,
+                     const int32_t* lens, int32_t clip_len, float* db, float* norm, float* zcr,
+                     uint8_t* img, uint32_t flags) {
+  if (!c) return MMLA_E_INVALID;
+  if (bad_pcm_args(pcm, n, stride, lens, clip_len)) return fail(c, MMLA_E_INVALID, "bad pcm args");
+  HIPCHK(c, hipSetDevice(c->device));
+  const bool dev = flags & MMLA_DEVICE_PTR;
+  const int64_t mb = dev ? std::max<int64_t>(n, 1) : c->od_mb;
+  for (int64_t c0 = 0; c0 < n; c0 += mb) {
+    const int64_t cnt = std::min(mb, n - c0);
+    Pcm p;
+    CHK(stage_pcm(c, pcm, c0, cnt, stride, lens, clip_len, MMLA_OD_CLIP, dev, &p));
+    OdFeArgs a{};
+    a.pcm = p.p;
+    a.clip_stride = p.stride;
+    a.lens = p.lens;
+    a.clip_len = p.clip_len;
+    a.tables = c->od_tables;
+    CHK(out_ptr(c, db, c0 * OD_PIX, cnt * OD_PIX, dev, S_OUT0, &a.db));
+    CHK(out_ptr(c, norm, c0 * OD_PIX, cnt * OD_PIX, dev, S_OUT1, &a.norm));
+    CHK(out_ptr(c, zcr, c0 * OD_W, cnt * OD_W, dev, S_OUT2, &a.zcr));
+    CHK(out_ptr(c, img, c0 * OD_IMG, cnt * OD_IMG, dev, S_OUT3, &a.img));
+    LAUNCH(c, MMLA_STAGE_OD_FE, od_fe_bytes(cnt, a), od_fe_launch(a, cnt, c->stream));
+    CHK(copy_back(c, db, c0 * OD_PIX, a.db, cnt * OD_PIX, dev));
+    CHK(copy_back(c, norm, c0 * OD_PIX, a.norm, cnt * OD_PIX, dev));
+    CHK(copy_back(c, zcr, c0 * OD_W, a.zcr, cnt * OD_W, dev));
+    CHK(copy_back(c, img, c0 * OD_IMG, a.img, cnt * OD_IMG, dev));
+    if (!dev) HIPCHK(c, hipStreamSynchronize(c->stream));
+  }
+  return finish(c, dev);
+}
+
+int mmla_si_features(mmla_ctx* c, const int16_t* pcm, int64_t n, int64_t stride,
+                     const int32_t* lens, int32_t clip_len, float* feat, uint8_t* silent,
+                     uint32_t flags) {
+  if (!c) return MMLA_E_INVALID;
+  if (bad_pcm_args(pcm, n, stride, lens, clip_len) || (n > 0 && !feat))
+    return fail(c, MMLA_E_INVALID, "bad pcm/feat args");
+  HIPCHK(c, hipSetDevice(c->device));
+  const bool dev = flags & MMLA_DEVICE_PTR;
+  const int64_t mb = dev ? std::max<int64_t>(n, 1) : c->si_mb;
+  for (int64_t c0 = 0; c0 < n; c0 += mb) {
+    const int64_t cnt = std::min(mb, n - c0);
+    Pcm p;
+    CHK(stage_pcm(c, pcm, c0, cnt, stride, lens, clip_len, SI_NEED_SAMPLES, dev, &p));
+    SiFeArgs a{};
+    a.pcm = p.p;
+    a.clip_stride = p.stride;
+    a.lens = p.lens;
+    a.clip_len = lens ? 0 : clip_len;   // true length decides T even if fewer samples are staged
+    a.tables = c->si_tables;
+    CHK(out_ptr(c, feat, c0 * SI_T * SI_D, cnt * SI_T * SI_D, dev, S_OUT0, &a.feat));
+    CHK(out_ptr(c, silent, c0, cnt, dev, S_OUT1, &a.silent));
+    LAUNCH(c, MMLA_STAGE_SI_FE, si_fe_bytes(cnt, a), si_fe_launch(a, cnt, c->stream));
+    CHK(copy_back(c, feat, c0 * SI_T * SI_D, a.feat, cnt * SI_T * SI_D, dev));
+    CHK(copy_back(c, silent, c0, a.silent, cnt, dev));
+    if (!dev) HIPCHK(c, hipStreamSynchronize(c->stream));
+  }
+  return finish(c, dev);
+}
+
+int mmla_si_features_seq(mmla_ctx* c, const int16_t* pcm, int64_t n_samples, int64_t n_windows,
+                         float* feat, uint32_t flags) {
+  if (!c) return MMLA_E_INVALID;
+  if (n_samples < 1 || !pcm || !feat) return fail(c, MMLA_E_INVALID, "bad si_features_seq args");
+  const int64_t T = n_samples <= 400 ? 1 : 1 + (n_samples - 400 + 159) / 160;
+  if (n_windows != (T + SI_T - 1) / SI_T)
+    return fail(c, MMLA_E_INVALID, "n_windows must be ceil(T/256) = %lld", (long long)((T + 255) / 256));
+  HIPCHK(c, hipSetDevice(c->device));
+  const bool dev = flags & MMLA_DEVICE_PTR;
+  const int16_t* dp = pcm;
+  if (!dev) {
+    void* p = nullptr;
+    CHK(ws_get(c, S_PCM, n_samples * sizeof(int16_t), &p));
+    HIPCHK(c, hipMemcpyAsync(p, pcm, n_samples * sizeof(int16_t), hipMemcpyHostToDevice, c->stream));
+    dp = static_cast<int16_t*>(p);
+  }
+  SiFeArgs a{};
+  a.pcm = dp;
+  a.seq_len = n_samples;
+  a.tables = c->si_tables;
+  CHK(out_ptr(c, feat, 0, n_windows * SI_T * SI_D, dev, S_OUT0, &a.feat));
+  LAUNCH(c, MMLA_STAGE_SI_FE, (double)n_samples * 2 + (double)n_windows * SI_T * SI_D * 4,
+         si_fe_launch(a, n_windows, c->stream));
+  CHK(copy_back(c, feat, 0, a.feat, n_windows * SI_T * SI_D, dev));
+  return finish(c, dev);
+}
+
+int mmla_od_forward(mmla_ctx* c, const float* x, int64_t n, float* probs, uint32_t flags) {
+  if (!c) return MMLA_E_INVALID;
+  if (n < 0 || (n > 0 && (!x || !probs))) return fail(c, MMLA_E_INVALID, "bad od_forward args");
+  if (!c->od_loaded) return fail(c, MMLA_E_NOWEIGHTS, "OD weights not loaded");
+  HIPCHK(c, hipSetDevice(c->device));
+  const bool dev = flags & MMLA_DEVICE_PTR;
+  for (int64_t c0 = 0; c0 < n; c0 += c->od_mb) {
+    const int64_t cnt = std::min(c->od_mb, n - c0);
+    const float* dx = x + c0 * OD_IMG;
+    if (!dev) {
+      void* p = nullptr;
+      CHK(ws_get(c, S_IN, cnt * OD_IMG * sizeof(float), &p));
+      HIPCHK(c, hipMemcpyAsync(p, dx, cnt * OD_IMG * sizeof(float), hipMemcpyHostToDevice, c->stream));
+      dx = static_cast<float*>(p);
+    }
+    float* dp;
+    CHK(out_ptr(c, probs, c0 * 2, cnt * 2, dev, S_OUT0, &dp));
+    CHK(run_od_net(c, nullptr, dx, cnt, dp, nullptr));
+    CHK(copy_back(c, probs, c0 * 2, dp, cnt * 2, dev));
+    if (!dev) HIPCHK(c, hipStreamSynchronize(c->stream));
+  }
+  return finish(c, dev);
+}
+
+int mmla_od_forward_u8(mmla_ctx* c, const uint8_t* img, int64_t n, float* probs, uint32_t flags) {
+  if (!c) return MMLA_E_INVALID;
+  if (n < 0 || (n > 0 && (!img || !probs))) return fail(c, MMLA_E_INVALID, "bad od_forward args");
+  if (!c->od_loaded) return fail(c, MMLA_E_NOWEIGHTS, "OD weights not loaded");
+  HIPCHK(c, hipSetDevice(c->device));
+  const bool dev = flags & MMLA_DEVICE_PTR;
+  for (int64_t c0 = 0; c0 < n; c0 += c->od_mb) {
+    const int64_t cnt = std::min(c->od_mb, n - c0);
+    const uint8_t* di = img + c0 * OD_IMG;
+    if (!dev) {
+      void* p = nullptr;
+      CHK(ws_get(c, S_IMG, cnt * OD_IMG, &p));
+      HIPCHK(c, hipMemcpyAsync(p, di, cnt * OD_IMG, hipMemcpyHostToDevice, c->stream));
+      di = static_cast<uint8_t*>(p);
+    }
+    float* dp;
+    CHK(out_ptr(c, probs, c0 * 2, cnt * 2, dev, S_OUT0, &dp));
+    CHK(run_od_net(c, di, nullptr, cnt, dp, nullptr));
+    CHK(copy_back(c, probs, c0 * 2, dp, cnt * 2, dev));
+    if (!dev) HIPCHK(c, hipStreamSynchronize(c->stream));
+  }
+  return finish(c, dev);
+}
+
+int mmla_si_forward(mmla_ctx* c, const float* x, int64_t n, float* probs, uint32_t flags) {
+  if (!c) return MMLA_E_INVALID;
+  if (n < 0 || (n > 0 && (!x || !probs))) return fail(c, MMLA_E_INVALID, "bad si_forward args");
+  if (!c->si_loaded) return fail(c, MMLA_E_NOWEIGHTS, "SI weights not loaded");
+  HIPCHK(c, hipSetDevice(c->device));
+  const bool dev = flags & MMLA_DEVICE_PTR;
+  const int k = c->si.k;
+  for (int64_t c0 = 0; c0 < n; c0 += c->si_mb) {
+    const int64_t cnt = std::min(c->si_mb, n - c0);
+    const float* dx = x + c0 * SI_T * SI_D;
+    if (!dev) {
+      void* p = nullptr;
+      CHK(ws_get(c, S_IN, cnt * SI_T * SI_D * sizeof(float), &p));
+      HIPCHK(c, hipMemcpyAsync(p, dx, cnt * SI_T * SI_D * sizeof(float), hipMemcpyHostToDevice,
+                               c->stream));
+      dx = static_cast<float*>(p);
+    }
+    float* dp;
+    CHK(out_ptr(c, probs, c0 * k, cnt * k, dev, S_OUT0, &dp));
+    CHK(run_si_net(c, dx, cnt, dp, nullptr, nullptr));
+    CHK(copy_back(c, probs, c0 * k, dp, cnt * k, dev));
+    if (!dev) HIPCHK(c, hipStreamSynchronize(c->stream));
+  }
+  return finish(c, dev);
+}
+
+int mmla_od_pipeline(mmla_ctx* c, const int16_t* pcm, int64_t n, int64_t stride,
+                     const int32_t* lens, int32_t clip_len, float* probs, int32_t* argmax,
+                     uint32_t flags) {
+  if (!c) return MMLA_E_INVALID;
+  if (bad_pcm_args(pcm, n, stride, lens, clip_len)) return fail(c, MMLA_E_INVALID, "bad pcm args");
+  if (!c->od_loaded) return fail(c, MMLA_E_NOWEIGHTS, "OD weights not loaded");
+  HIPCHK(c, hipSetDevice(c->device));
+  const bool dev = flags & MMLA_DEVICE_PTR;
+  for (int64_t c0 = 0; c0 < n; c0 += c->od_mb) {
+    const int64_t cnt = std::min(c->od_mb, n - c0);
+    Pcm p;
+    CHK(stage_pcm(c, pcm, c0, cnt, stride, lens, clip_len, MMLA_OD_CLIP, dev, &p));
+    void* pimg = nullptr;
+    CHK(ws_get(c, S_IMG, cnt * OD_IMG, &pimg));
+    OdFeArgs a{};
+    a.pcm = p.p;
+    a.clip_stride = p.stride;
+    a.lens = p.lens;
+    a.clip_len = p.clip_len;
+    a.tables = c->od_tables;
+    a.img = static_cast<uint8_t*>(pimg);
+    LAUNCH(c, MMLA_STAGE_OD_FE, od_fe_bytes(cnt, a), od_fe_launch(a, cnt, c->stream));
+    float* dp;
+    int32_t* da;
+    CHK(out_ptr(c, probs, c0 * 2, cnt * 2, dev, S_OUT0, &dp));
+    CHK(out_ptr(c, argmax, c0, cnt, dev, S_OUT1, &da));
+    CHK(run_od_net(c, a.img, nullptr, cnt, dp, da));
+    CHK(copy_back(c, probs, c0 * 2, dp, cnt * 2, dev));
+    CHK(copy_back(c, argmax, c0, da, cnt, dev));
+    if (!dev) HIPCHK(c, hipStreamSynchronize(c->stream));
+  }
+  return finish(c, dev);
+}
+
+int mmla_si_pipeline(mmla_ctx* c, const int16_t* pcm, int64_t n, int64_t stride,
+                     const int32_t* lens, int32_t clip_len, float* probs, int32_t* argmax,
+                     uint8_t* silent, uint32_t flags) {
+  if (!c) return MMLA_E_INVALID;
+  if (bad_pcm_args(pcm, n, stride, lens, clip_len)) return fail(c, MMLA_E_INVALID, "bad pcm args");
+  if (!c->si_loaded) return fail(c, MMLA_E_NOWEIGHTS, "SI weights not loaded");
+  HIPCHK(c, hipSetDevice(c->device));
+  const bool dev = flags & MMLA_DEVICE_PTR;
+  const int k = c->si.k;
+  for (int64_t c0 = 0; c0 < n; c0 += c->si_mb) {
+    const int64_t cnt = std::min(c->si_mb, n - c0);
+    Pcm p;
+    CHK(stage_pcm(c, pcm, c0, cnt, stride, lens, clip_len, SI_NEED_SAMPLES, dev, &p));
+    void *pf, *ps;
+    CHK(ws_get(c, S_FEAT, cnt * SI_T * SI_D * sizeof(float), &pf));
+    CHK(ws_get(c, S_SILENT, cnt, &ps));
+    SiFeArgs a{};
+    a.pcm = p.p;
+    a.clip_stride = p.stride;
+    a.lens = p.lens;
+    a.clip_len = lens ? 0 : clip_len;
+    a.tables = c->si_tables;
+    a.feat = static_cast<float*>(pf);
+    a.silent = static_cast<uint8_t*>(ps);
+    LAUNCH(c, MMLA_STAGE_SI_FE, si_fe_bytes(cnt, a), si_fe_launch(a, cnt, c->stream));
+    float* dp;
+    int32_t* da;
+    CHK(out_ptr(c, probs, c0 * k, cnt * k, dev, S_OUT0, &dp));
+    CHK(out_ptr(c, argmax, c0, cnt, dev, S_OUT1, &da));
+    CHK(run_si_net(c, a.feat, cnt, dp, da, a.silent));
+    CHK(copy_back(c, probs, c0 * k, dp, cnt * k, dev));
+    CHK(copy_back(c, argmax, c0, da, cnt, dev));
+    if (silent) {
+      if (dev)
+        HIPCHK(c, hipMemcpyAsync(silent + c0, a.silent, cnt, hipMemcpyDeviceToDevice, c->stream));
+      else
+        HIPCHK(c, hipMemcpyAsync(silent + c0, a.silent, cnt, hipMemcpyDeviceToHost, c->stream));
+    }
+    if (!dev) HIPCHK(c, hipStreamSynchronize(c->stream));
+  }
+  return finish(c, dev);
+}
+
+int mmla_profile_enable(mmla_ctx* c, int on) {
+  if (!c) return MMLA_E_INVALID;
+  c->prof_on = on != 0;
+  return MMLA_OK;
+}
+
+int mmla_profile_read(mmla_ctx* c, double* ms, int64_t* launches, double* work, int reset) {
+  if (!c) return MMLA_E_INVALID;
+  CHK(prof_collect(c));
+  for (int i = 0; i < MMLA_NSTAGES; ++i) {
+    if (ms) ms[i] = c->prof_ms[i];
+    if (launches) launches[i] = c->prof_n[i];
+    if (work) work[i] = c->prof_work[i];
+    if (reset) {
+      c->prof_ms[i] = 0.0;
+      c->prof_n[i] = 0;
+      c->prof_work[i] = 0.0;
+    }
+  }
+  return MMLA_OK;
+}
+
+}  // extern "C"

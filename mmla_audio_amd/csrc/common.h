@@ -1,0 +1,49 @@
+// Shared device helpers for the mmla HIP kernels (gfx950 / CDNA4, wave64).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define MMLA_DEV __device__ __forceinline__
+
+struct cf {  // complex float held in two VGPRs
+  float x, y;
+};
+MMLA_DEV cf cadd(cf a, cf b) { return {a.x + b.x, a.y + b.y}; }
+MMLA_DEV cf csub(cf a, cf b) { return {a.x - b.x, a.y - b.y}; }
+MMLA_DEV cf cmul(cf a, cf b) { return {a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x}; }
+MMLA_DEV cf cconj(cf a) { return {a.x, -a.y}; }
+MMLA_DEV cf cmul_negi(cf a) { return {a.y, -a.x}; }  // -i * a
+MMLA_DEV cf cscale(cf a, float s) { return {a.x * s, a.y * s}; }
+
+struct cd {  // complex double
+  double x, y;
+};
+MMLA_DEV cd cadd(cd a, cd b) { return {a.x + b.x, a.y + b.y}; }
+MMLA_DEV cd csub(cd a, cd b) { return {a.x - b.x, a.y - b.y}; }
+MMLA_DEV cd cmul(cd a, cd b) { return {a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x}; }
+MMLA_DEV cd cconj(cd a) { return {a.x, -a.y}; }
+MMLA_DEV cd cmul_negi(cd a) { return {a.y, -a.x}; }
+MMLA_DEV cd cscale(cd a, double s) { return {a.x * s, a.y * s}; }
+
+template <typename T>
+MMLA_DEV T wave_max(T v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+  return v;
+}
+template <typename T>
+MMLA_DEV T wave_min(T v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, 64));
+  return v;
+}
+template <typename T>
+MMLA_DEV T wave_sum(T v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Kernel launch wrappers are declared extern "C++" here and defined in the .hip files; the C ABI
+// (capi.cpp) calls them.
+struct OdFeTables;  // device constant tables for the OD front-end

@@ -1,0 +1,29 @@
+// Small network kernels around the conv GEMM: OD stem, pooling/reduction glue, BiLSTM, heads.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+// OD stem Conv2D 1x1 3->16 on the decoded PNG (uint8) or a float NHWC input.
+hipError_t od_stem_launch(const uint8_t* img_u8, const float* img_f32, int64_t n_pix,
+                          const float* w /*[3][16]*/, const float* b /*[16]*/, float* y,
+                          hipStream_t s);
+// Lambda(K.mean(x, axis=1)): [n, h, w, c] -> [n, w, c]
+hipError_t mean_h_launch(const float* x, int n, int h, int w, int c, float* y, hipStream_t s);
+// MaxPool1D(2, 'same') on [n, t, c] -> [n, ceil(t/2), c]
+hipError_t maxpool_t2_launch(const float* x, int n, int t, int c, float* y, hipStream_t s);
+// SI tail: BatchNorm -> ReLU -> AveragePooling1D(4) on [n, t, c] -> [n, t/4, c]
+hipError_t bn_relu_avgpool4_launch(const float* x, int n, int t, int c, const float* scale,
+                                   const float* shift, float* y, hipStream_t s);
+// Bidirectional(LSTM(256), merge 'concat') last state.  seq [n, T, D]; wcat[dir] =
+// [(256 + D) x 1024] (recurrent kernel rows first, then input kernel rows); bias[dir] [1024];
+// out [n, 512] = [h_fwd(T-1), h_bwd(after x[0])].
+hipError_t bilstm_launch(const float* seq, int n, int T, int D, const float* wcat_fwd,
+                         const float* wcat_bwd, const float* bias_fwd, const float* bias_bwd,
+                         float* out, hipStream_t s);
+// OD head: LeakyReLU(0.3) -> Dense(512 -> 2) -> softmax; probs [n,2], argmax [n] (nullable)
+hipError_t od_head_launch(const float* h, int n, const float* w /*[512][2]*/, const float* b,
+                          float* probs, int32_t* argmax, hipStream_t s);
+// SI head activation on logits [n, ld]: softmax (head 0) or sigmoid (head 1) over the first k;
+// argmax [n] (-1 where silent[i] != 0).
+hipError_t si_head_launch(const float* logits, int n, int k, int ld, int head, float* probs,
+                          int32_t* argmax, const uint8_t* silent, hipStream_t s);

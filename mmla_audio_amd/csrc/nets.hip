@@ -1,0 +1,300 @@
+// Network glue kernels: OD stem, Lambda mean, MaxPool1D, SI BN+ReLU+AvgPool, BiLSTM, heads.
+//
+// BiLSTM (Keras 2.6 LSTM, gates i,f,c,o, sigmoid/tanh, h0 = c0 = 0; Bidirectional concat of the
+// last states -- overlap_detector_temp.py:297, speaker_identification.py:213) runs as one launch per
+// layer: a workgroup owns 32 clips of one direction for all T steps.  Each step is one f32-MFMA
+// product [32 x (256 + D)] x [(256 + D) x 1024] with A = [h_{t-1} | x_t] staged in LDS and B (the
+// stacked recurrent + input kernels, 1.5 MB, L2-resident) streamed from global; wave w owns hidden
+// units [64w, 64w+64) for all four gates, so the gate math and the c-state stay in registers.
+#include "common.h"
+#include "nets.h"
+
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+template <typename T>
+__global__ void od_stem_kernel(const T* __restrict__ x, int64_t n_pix, const float* __restrict__ w,
+                               const float* __restrict__ b, float* __restrict__ y) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;   // (pixel, output quad)
+  if (i >= n_pix * 4) return;
+  const int64_t p = i >> 2;
+  const int q = (int)(i & 3);
+  const float x0 = (float)x[p * 3 + 0], x1 = (float)x[p * 3 + 1], x2 = (float)x[p * 3 + 2];
+  float4 o;
+  float* op = &o.x;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int co = q * 4 + j;
+    // Keras Conv2D 1x1: sum over ci in order, then bias
+    float acc = x0 * w[0 * 16 + co];
+    acc = fmaf(x1, w[1 * 16 + co], acc);
+    acc = fmaf(x2, w[2 * 16 + co], acc);
+    op[j] = acc + b[co];
+  }
+  reinterpret_cast<float4*>(y)[i] = o;
+}
+
+__global__ void mean_h_kernel(const float* __restrict__ x, int n, int h, int w, int c,
+                              float* __restrict__ y) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;   // over n*w*c
+  const int64_t tot = (int64_t)n * w * c;
+  if (i >= tot) return;
+  const int ci = (int)(i % c);
+  const int64_t r = i / c;
+  const int wi = (int)(r % w);
+  const int64_t ni = r / w;
+  float s = 0.0f;
+  for (int hh = 0; hh < h; ++hh) s += x[((ni * h + hh) * w + wi) * c + ci];
+  y[i] = s / (float)h;
+}
+
+__global__ void maxpool_t2_kernel(const float* __restrict__ x, int n, int t, int c,
+                                  float* __restrict__ y) {
+  const int to = (t + 1) / 2;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t tot = (int64_t)n * to * c;
+  if (i >= tot) return;
+  const int ci = (int)(i % c);
+  const int64_t r = i / c;
+  const int ti = (int)(r % to);
+  const int64_t ni = r / to;
+  float m = x[(ni * t + 2 * ti) * c + ci];
+  if (2 * ti + 1 < t) m = fmaxf(m, x[(ni * t + 2 * ti + 1) * c + ci]);
+  y[i] = m;
+}
+
+__global__ void bn_relu_avgpool4_kernel(const float* __restrict__ x, int n, int t, int c,
+                                        const float* __restrict__ sc, const float* __restrict__ sh,
+                                        float* __restrict__ y) {
+  const int to = t / 4;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t tot = (int64_t)n * to * c;
+  if (i >= tot) return;
+  const int ci = (int)(i % c);
+  const int64_t r = i / c;
+  const int ti = (int)(r % to);
+  const int64_t ni = r / to;
+  float s = 0.0f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) s += fmaxf(fmaf(x[(ni * t + 4 * ti + j) * c + ci], sc[ci], sh[ci]), 0.0f);
+  y[i] = s / 4.0f;
+}
+
+MMLA_DEV float sigm(float z) { return 1.0f / (1.0f + expf(-z)); }
+
+constexpr int LSTM_U = 256;
+constexpr int LSTM_ROWS = 32;
+
+template <int D>
+__global__ void __launch_bounds__(256) bilstm_kernel(const float* __restrict__ seq, int n, int T,
+                                                     const float* __restrict__ wf,
+                                                     const float* __restrict__ wb,
+                                                     const float* __restrict__ bf,
+                                                     const float* __restrict__ bb,
+                                                     float* __restrict__ out) {
+  constexpr int K = LSTM_U + D;
+  constexpr int LDH = K + 1;
+  __shared__ float Ah[LSTM_ROWS][LDH];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int dir = blockIdx.y;
+  const float* __restrict__ W = dir == 0 ? wf : wb;
+  const float* __restrict__ B = dir == 0 ? bf : bb;
+  const int64_t c0 = (int64_t)blockIdx.x * LSTM_ROWS;
+
+  for (int e = tid; e < LSTM_ROWS * LSTM_U; e += 256) Ah[e / LSTM_U][e % LSTM_U] = 0.0f;
+  float cst[2][16];
+#pragma unroll
+  for (int ht = 0; ht < 2; ++ht)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) cst[ht][r] = 0.0f;
+
+  const int col_base = 64 * wave + (lane & 31);   // + 32*ht + 256*g
+  const int khalf = lane >> 5;
+
+  for (int s = 0; s < T; ++s) {
+    const int t = dir == 0 ? s : T - 1 - s;
+    for (int e = tid; e < LSTM_ROWS * D; e += 256) {
+      const int r = e / D, d = e - r * D;
+      const int64_t clip = c0 + r;
+      Ah[r][LSTM_U + d] = clip < n ? seq[(clip * T + t) * D + d] : 0.0f;
+    }
+    __syncthreads();
+    f32x16 acc[4][2];
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int ht = 0; ht < 2; ++ht) {
+        const float bv = B[g * LSTM_U + col_base + 32 * ht];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[g][ht][r] = bv;
+      }
+    const float* wp = W + (int64_t)khalf * 1024 + col_base;
+#pragma unroll 4
+    for (int k2 = 0; k2 < K / 2; ++k2) {
+      const float av = Ah[lane & 31][2 * k2 + khalf];
+      const float* wr = wp + (int64_t)(2 * k2) * 1024;
+      float bv[4][2];
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int ht = 0; ht < 2; ++ht) bv[g][ht] = wr[g * LSTM_U + 32 * ht];
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int ht = 0; ht < 2; ++ht)
+          acc[g][ht] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv[g][ht], acc[g][ht], 0, 0, 0);
+    }
+    __syncthreads();   // every wave has read h_{t-1}
+#pragma unroll
+    for (int ht = 0; ht < 2; ++ht)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        const float ig = sigm(acc[0][ht][r]);
+        const float fg = sigm(acc[1][ht][r]);
+        const float gg = tanhf(acc[2][ht][r]);
+        const float og = sigm(acc[3][ht][r]);
+        const float c = fg * cst[ht][r] + ig * gg;
+        cst[ht][r] = c;
+        Ah[row][col_base + 32 * ht] = og * tanhf(c);
+      }
+    __syncthreads();
+  }
+  for (int e = tid; e < LSTM_ROWS * LSTM_U; e += 256) {
+    const int r = e / LSTM_U, j = e - r * LSTM_U;
+    const int64_t clip = c0 + r;
+    if (clip < n) out[clip * 512 + dir * LSTM_U + j] = Ah[r][j];
+  }
+}
+
+__global__ void od_head_kernel(const float* __restrict__ h, int n, const float* __restrict__ w,
+                               const float* __restrict__ b, float* __restrict__ probs,
+                               int32_t* __restrict__ argmax) {
+  // one wave per clip
+  const int lane = threadIdx.x & 63;
+  const int64_t clip = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (clip >= n) return;
+  const float alpha = 0.30000001192092896f;   // LeakyReLU(alpha=0.3) stored float32
+  float z0 = 0.0f, z1 = 0.0f;
+  for (int i = lane; i < 512; i += 64) {
+    float v = h[clip * 512 + i];
+    v = v > 0.0f ? v : v * alpha;
+    z0 = fmaf(v, w[i * 2 + 0], z0);
+    z1 = fmaf(v, w[i * 2 + 1], z1);
+  }
+  z0 = wave_sum(z0) + b[0];
+  z1 = wave_sum(z1) + b[1];
+  if (lane == 0) {
+    const float m = fmaxf(z0, z1);
+    const float e0 = expf(z0 - m), e1 = expf(z1 - m);
+    const float s = e0 + e1;
+    if (probs) {
+      probs[clip * 2 + 0] = e0 / s;
+      probs[clip * 2 + 1] = e1 / s;
+    }
+    if (argmax) argmax[clip] = e1 / s > e0 / s ? 1 : 0;
+  }
+}
+
+__global__ void si_head_kernel(const float* __restrict__ logits, int n, int k, int ld, int head,
+                               float* __restrict__ probs, int32_t* __restrict__ argmax,
+                               const uint8_t* __restrict__ silent) {
+  const int lane = threadIdx.x & 63;
+  const int64_t clip = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (clip >= n) return;
+  const float* z = logits + clip * ld;
+  float m = -INFINITY;
+  for (int i = lane; i < k; i += 64) m = fmaxf(m, z[i]);
+  m = wave_max(m);
+  float s = 0.0f;
+  if (head == 0) {
+    for (int i = lane; i < k; i += 64) s += expf(z[i] - m);
+    s = wave_sum(s);
+  }
+  float best = -INFINITY;
+  int bi = 0x7fffffff;
+  for (int i = lane; i < k; i += 64) {
+    const float p = head == 0 ? expf(z[i] - m) / s : 1.0f / (1.0f + expf(-z[i]));
+    if (probs) probs[clip * k + i] = p;
+    if (p > best) {   // first occurrence within the lane's strided subset
+      best = p;
+      bi = i;
+    }
+  }
+  // wave argmax, ties -> lowest index (numpy argmax)
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ob = __shfl_xor(best, o, 64);
+    const int oi = __shfl_xor(bi, o, 64);
+    if (ob > best || (ob == best && oi < bi)) {
+      best = ob;
+      bi = oi;
+    }
+  }
+  if (lane == 0 && argmax) argmax[clip] = (silent && silent[clip]) ? -1 : bi;
+}
+
+inline unsigned blocks_for(int64_t work, int bs) { return (unsigned)((work + bs - 1) / bs); }
+
+}  // namespace
+
+hipError_t od_stem_launch(const uint8_t* img_u8, const float* img_f32, int64_t n_pix,
+                          const float* w, const float* b, float* y, hipStream_t s) {
+  if (n_pix <= 0) return hipSuccess;
+  if (img_u8)
+    hipLaunchKernelGGL(od_stem_kernel<uint8_t>, dim3(blocks_for(n_pix * 4, 256)), dim3(256), 0, s,
+                       img_u8, n_pix, w, b, y);
+  else
+    hipLaunchKernelGGL(od_stem_kernel<float>, dim3(blocks_for(n_pix * 4, 256)), dim3(256), 0, s,
+                       img_f32, n_pix, w, b, y);
+  return hipGetLastError();
+}
+
+hipError_t mean_h_launch(const float* x, int n, int h, int w, int c, float* y, hipStream_t s) {
+  const int64_t tot = (int64_t)n * w * c;
+  if (tot <= 0) return hipSuccess;
+  hipLaunchKernelGGL(mean_h_kernel, dim3(blocks_for(tot, 256)), dim3(256), 0, s, x, n, h, w, c, y);
+  return hipGetLastError();
+}
+
+hipError_t maxpool_t2_launch(const float* x, int n, int t, int c, float* y, hipStream_t s) {
+  const int64_t tot = (int64_t)n * ((t + 1) / 2) * c;
+  if (tot <= 0) return hipSuccess;
+  hipLaunchKernelGGL(maxpool_t2_kernel, dim3(blocks_for(tot, 256)), dim3(256), 0, s, x, n, t, c, y);
+  return hipGetLastError();
+}
+
+hipError_t bn_relu_avgpool4_launch(const float* x, int n, int t, int c, const float* scale,
+                                   const float* shift, float* y, hipStream_t s) {
+  const int64_t tot = (int64_t)n * (t / 4) * c;
+  if (tot <= 0) return hipSuccess;
+  hipLaunchKernelGGL(bn_relu_avgpool4_kernel, dim3(blocks_for(tot, 256)), dim3(256), 0, s, x, n, t,
+                     c, scale, shift, y);
+  return hipGetLastError();
+}
+
+hipError_t bilstm_launch(const float* seq, int n, int T, int D, const float* wf, const float* wb,
+                         const float* bf, const float* bb, float* out, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  if (D != 128) return hipErrorInvalidValue;
+  dim3 grid(blocks_for(n, LSTM_ROWS), 2);
+  hipLaunchKernelGGL(bilstm_kernel<128>, grid, dim3(256), 0, s, seq, n, T, wf, wb, bf, bb, out);
+  return hipGetLastError();
+}
+
+hipError_t od_head_launch(const float* h, int n, const float* w, const float* b, float* probs,
+                          int32_t* argmax, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(od_head_kernel, dim3(blocks_for((int64_t)n * 64, 256)), dim3(256), 0, s, h, n,
+                     w, b, probs, argmax);
+  return hipGetLastError();
+}
+
+hipError_t si_head_launch(const float* logits, int n, int k, int ld, int head, float* probs,
+                          int32_t* argmax, const uint8_t* silent, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(si_head_kernel, dim3(blocks_for((int64_t)n * 64, 256)), dim3(256), 0, s,
+                     logits, n, k, ld, head, probs, argmax, silent);
+  return hipGetLastError();
+}

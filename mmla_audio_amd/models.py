@@ -1,0 +1,112 @@
+"""``load_model(path).predict(x)`` facade for the two reference networks.
+
+Replaces ``tf.keras.models.load_model`` + ``Model.predict`` at the reference call sites
+(OD ``record_on_pc.py:88,159``; SI ``record_on_pc.py:77,136``;
+``speaker_identification_post_processing.py:206,272``; ``overlap_detection_post_processing.py``).
+
+Weights: if ``<path>/variables/variables.data-00000-of-00001`` exists the trained tensors are read
+from the TF bundle (``tfbundle.load_bundle``); the reference does not ship that file
+(``.MISSING_LARGE_BLOBS``), so otherwise seeded synthetic weights in the exact reference layout are
+used and ``model.synthetic`` is True.
+"""
+import os
+import warnings
+
+import numpy as np
+
+from . import _lib, tfbundle, weights
+
+
+def _kind_from_path(path):
+    idx = os.path.join(path, 'variables', 'variables.index')
+    if os.path.exists(idx):
+        shapes = tfbundle.variable_shapes(idx)
+        k0 = shapes.get('layer_with_weights-0/kernel')
+        if k0 is not None:
+            return weights.OD if len(k0) == 4 else weights.SI
+    low = path.replace('\\', '/').lower()
+    return weights.OD if 'overlap' in low or 'timit2' in low or 'timit1' in low else weights.SI
+
+
+class _Model:
+    kind = None
+
+    def __init__(self, W, n_classes, head, device=None, synthetic=False):
+        self.ctx = _lib.default_context(device) if device is None or isinstance(device, int) else device
+        self.n_classes = n_classes
+        self.head = head
+        self.synthetic = synthetic
+        self.W = W
+        self.ctx.load_weights(self.kind, weights.pack(self.kind, W, n_classes), n_classes, head)
+
+    def _ensure_loaded(self):
+        # several models can share one context; re-load if another model of this kind replaced ours
+        cls = self.ctx.od_classes if self.kind == weights.OD else self.ctx.si_classes
+        if getattr(self.ctx, f'_owner_{self.kind}', None) is not self or cls != self.n_classes:
+            self.ctx.load_weights(self.kind, weights.pack(self.kind, self.W, self.n_classes),
+                                  self.n_classes, self.head)
+            setattr(self.ctx, f'_owner_{self.kind}', self)
+
+
+class OverlapDetectionModel(_Model):
+    """OD-NET (ResLSTM, overlap_detector_temp.py:280-303): predict(float32 [N,128,151,3]) -> [N,2]."""
+    kind = weights.OD
+
+    def __init__(self, W, device=None, synthetic=False):
+        super().__init__(W, 2, _lib.HEAD_SOFTMAX, device, synthetic)
+        setattr(self.ctx, f'_owner_{self.kind}', self)
+
+    def predict(self, x, batch_size=None, verbose=0):
+        self._ensure_loaded()
+        x = np.asarray(x)
+        if x.ndim != 4 or x.shape[1:] != (128, 151, 3):
+            raise ValueError(f'OD model expects [N,128,151,3], got {x.shape}')
+        return self.ctx.od_forward(x)
+
+    def predict_wavs(self, pcm, lens=None):
+        """Fused WAV -> class (no PNG round trip): int16 [N, L] -> (probs [N,2], argmax [N])."""
+        self._ensure_loaded()
+        return self.ctx.od_pipeline(pcm, lens)
+
+
+class SpeakerIdModel(_Model):
+    """SI-NET (res_model + head, speaker_identification.py:193-218,401-410): predict([N,256,39])."""
+    kind = weights.SI
+
+    def __init__(self, W, n_classes, head, device=None, synthetic=False):
+        super().__init__(W, n_classes, head, device, synthetic)
+        setattr(self.ctx, f'_owner_{self.kind}', self)
+
+    def predict(self, x, batch_size=None, verbose=0):
+        self._ensure_loaded()
+        x = np.asarray(x)
+        if x.ndim != 3 or x.shape[1:] != (256, 39):
+            raise ValueError(f'SI model expects [N,256,39], got {x.shape}')
+        return self.ctx.si_forward(x)
+
+    def predict_wavs(self, pcm, lens=None):
+        """Fused WAV -> speaker: -> (probs [N,K], argmax [N] (-1 = 'silent'), silent [N])."""
+        self._ensure_loaded()
+        return self.ctx.si_pipeline(pcm, lens)
+
+
+def load_model(path, kind=None, n_classes=None, head=None, seed=0, device=None):
+    """tf.keras.models.load_model drop-in for the two reference model directories."""
+    kind = _kind_from_path(path) if kind is None else kind
+    synthetic = False
+    try:
+        W = tfbundle.load_bundle(path, 40 if kind == weights.OD else 41)
+        if kind == weights.SI:
+            n_classes = W['layer_with_weights-42/kernel'].shape[1]
+    except (FileNotFoundError, OSError):
+        warnings.warn(f'{path}: trained weights absent (reference .MISSING_LARGE_BLOBS); using seeded '
+                      f'synthetic weights in the reference layout (seed={seed})')
+        W = weights.synthetic(kind, seed=seed, n_classes=n_classes)
+        synthetic = True
+    if kind == weights.OD:
+        return OverlapDetectionModel(W, device=device, synthetic=synthetic)
+    if n_classes is None:
+        n_classes = W['layer_with_weights-42/kernel'].shape[1]
+    if head is None:
+        head = _lib.HEAD_SOFTMAX if n_classes == 630 else _lib.HEAD_SIGMOID
+    return SpeakerIdModel(W, n_classes, head, device=device, synthetic=synthetic)

@@ -1,0 +1,196 @@
+"""GPU parity: the HIP path through the C ABI against the oracle and the golden fixtures.
+
+Tolerances (BASELINE.json north_star):
+  OD normalised log-mel   max-abs <= 1e-4 (float32 FFT vs librosa's float64 FFT)
+  OD dB                   max-abs <= 5e-3 dB (same source; dB is not the model input)
+  OD ZCR                  exact integer crossing counts
+  OD image (model input)  R exact; G/B <= 1 LSB on <= 1e-3 of pixels
+  SI features             max-abs <= 1e-4 on [256, 39] (float64 kernel, float32 store)
+  nets                    probabilities max-abs <= 1e-4 vs a float64 numpy restatement;
+                          argmax identical except near-ties |p_a - p_b| < 1e-4
+"""
+import numpy as np
+import pytest
+
+from oracle import nets, od_fe, si_fe, synth
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope='module')
+def ctx():
+    from mmla_audio_amd import _lib
+    return _lib.Context(0)
+
+
+def _od_compare(f, i, ref, tag):
+    nan = np.isnan(ref['norm'])
+    assert np.array_equal(np.isnan(f['norm'][i]), nan), tag
+    if (~nan).any():
+        err = np.abs(f['norm'][i][~nan] - ref['norm'][~nan]).max()
+        assert err <= 1e-4, f'{tag}: norm err {err}'
+        derr = np.abs(f['db'][i] - ref['db']).max()
+        assert derr <= 5e-3, f'{tag}: dB err {derr}'
+    counts = np.rint(f['zcr'][i] * 400).astype(int)
+    assert np.array_equal(counts, np.rint(ref['zcr'][0] * 400).astype(int)), tag
+    assert np.abs(f['zcr'][i] - ref['zcr'][0]).max() < 1e-7
+    img = f['img'][i].astype(int)
+    want = ref['png_rgb'].astype(int)
+    assert np.array_equal(img[..., 0], want[..., 0]), f'{tag}: R channel'
+    d = np.abs(img - want)
+    assert d.max() <= 1 and np.count_nonzero(d) <= 1e-3 * d.size, f'{tag}: {np.count_nonzero(d)} px'
+
+
+def test_od_features_golden(ctx, od_golden):
+    names = list(od_golden['names'])
+    pcms = [od_golden[f'pcm_{i}'] for i in range(len(names))]
+    f = ctx.od_features(pcms)
+    for i, name in enumerate(names):
+        ref = {'norm': od_golden[f'norm_{i}'], 'db': od_golden[f'db_{i}'],
+               'zcr': od_golden[f'zcr_{i}'], 'png_rgb': od_golden[f'png_{i}']}
+        _od_compare(f, i, ref, name)
+
+
+def test_od_features_synthetic_batch(ctx):
+    pcm = synth.batch(100, 40, 40000)
+    f = ctx.od_features(pcm)
+    for i in range(len(pcm)):
+        _od_compare(f, i, od_fe.od_features(pcm[i]), f'clip{100 + i}')
+
+
+def test_od_features_ragged_lengths(ctx):
+    lens = [0, 1, 399, 400, 4000, 16000, 23999, 24000, 24001, 40000]
+    pcm = [synth.clip(200 + i, n) if n else np.zeros(0, np.int16) for i, n in enumerate(lens)]
+    f = ctx.od_features(pcm)
+    for i, p in enumerate(pcm):
+        _od_compare(f, i, od_fe.od_features(p), f'len{lens[i]}')
+
+
+def test_si_features_golden(ctx, si_golden):
+    names = list(si_golden['names'])
+    pcms = [si_golden[f'pcm_{i}'] for i in range(len(names))]
+    feat, silent = ctx.si_features(pcms)
+    for i, name in enumerate(names):
+        assert bool(silent[i]) == bool(si_golden[f'silent_{i}']), name
+        want = si_golden[f'feat_{i}'][0]
+        err = np.abs(feat[i] - want).max()
+        assert err <= 1e-4, f'{name}: SI err {err}'
+
+
+def test_si_features_synthetic(ctx):
+    lens = [3999, 4000, 4001, 24000, 24000, 24000, 40000, 40960, 41200, 41840, 42000, 48000, 80000]
+    pcm = [synth.clip(300 + i, n) for i, n in enumerate(lens)]
+    feat, silent = ctx.si_features(pcm)
+    for i, p in enumerate(pcm):
+        ref = si_fe.input_feature_gen(p)
+        if isinstance(ref, str):
+            assert silent[i] and not feat[i].any()
+            continue
+        err = np.abs(feat[i] - ref[0]).max()
+        assert err <= 1e-4, f'len {lens[i]}: SI err {err}'
+
+
+def test_si_features_sequence_mode(ctx):
+    sig = np.concatenate([synth.clip(400 + i, 40000) for i in range(5)])   # 12.5 s, 1248 frames
+    ref = si_fe.conversation_chunks(sig)
+    got = ctx.si_features_seq(sig)
+    assert got.shape == ref.shape
+    assert np.abs(got - ref).max() <= 1e-4
+
+
+def _near_tie_ok(p_gpu, p_ref):
+    a = p_gpu.argmax(1)
+    b = p_ref.argmax(1)
+    srt = np.sort(p_ref, axis=1)
+    tie = (srt[:, -1] - srt[:, -2]) < 1e-4
+    return np.all((a == b) | tie)
+
+
+def test_od_forward_vs_oracle(ctx, od_golden):
+    from mmla_audio_amd import weights
+    W = weights.synthetic(weights.OD, seed=1)
+    ctx.load_weights(weights.OD, weights.pack(weights.OD, W), 2)
+    rng = np.random.default_rng(3)
+    x = np.concatenate([np.stack([od_golden[f'png_{i}'] for i in range(len(od_golden['names']))]),
+                        rng.integers(0, 256, size=(5, 128, 151, 3))]).astype(np.float32)
+    p = ctx.od_forward(x)
+    ref = nets.od_forward(x, W)
+    assert np.abs(p - ref).max() <= 1e-4, np.abs(p - ref).max()
+    assert _near_tie_ok(p, ref)
+    p8 = ctx.od_forward(x.astype(np.uint8))
+    assert np.array_equal(p8, p)
+
+
+@pytest.mark.parametrize('k,head', [(630, 0), (8, 1), (1, 1)])
+def test_si_forward_vs_oracle(ctx, si_golden, k, head):
+    from mmla_audio_amd import weights
+    W = weights.synthetic(weights.SI, seed=2, n_classes=k)
+    ctx.load_weights(weights.SI, weights.pack(weights.SI, W, k), k, head)
+    x = np.stack([si_golden[f'feat_{i}'][0] for i in range(len(si_golden['names']))])
+    x = np.concatenate([x, np.random.default_rng(5).standard_normal((9, 256, 39)) * 10])
+    p = ctx.si_forward(x.astype(np.float32))
+    ref = nets.si_forward(x.astype(np.float32), W, head='softmax' if head == 0 else 'sigmoid')
+    assert p.shape == (len(x), k)
+    assert np.abs(p - ref).max() <= 1e-4, np.abs(p - ref).max()
+    if k > 1:
+        assert _near_tie_ok(p, ref)
+
+
+def test_od_pipeline_matches_features_then_forward(ctx):
+    from mmla_audio_amd import weights
+    W = weights.synthetic(weights.OD, seed=4)
+    ctx.load_weights(weights.OD, weights.pack(weights.OD, W), 2)
+    pcm = synth.batch(500, 12, 40000)
+    probs, am = ctx.od_pipeline(pcm)
+    f = ctx.od_features(pcm, db=False, norm=False, zcr=False)
+    p2 = ctx.od_forward(f['img'])
+    assert np.array_equal(probs, p2)
+    assert np.array_equal(am, probs.argmax(1))
+    ref = nets.od_forward(f['img'].astype(np.float32), W)
+    assert np.abs(probs - ref).max() <= 1e-4
+    # end to end against the oracle front-end too (image may differ by 1 LSB on a few pixels)
+    ref_img = np.stack([od_fe.od_features(p)['png_rgb'] for p in pcm]).astype(np.float32)
+    ref2 = nets.od_forward(ref_img, W)
+    assert np.abs(probs - ref2).max() <= 1e-3
+    assert _near_tie_ok(probs, ref2)
+
+
+def test_si_pipeline_silent_and_argmax(ctx):
+    from mmla_audio_amd import weights
+    W = weights.synthetic(weights.SI, seed=6, n_classes=8)
+    ctx.load_weights(weights.SI, weights.pack(weights.SI, W, 8), 8, 1)
+    lens = [24000, 3000, 24000, 40960, 100, 24000]
+    pcm = [synth.clip(600 + i, n) for i, n in enumerate(lens)]
+    probs, am, silent = ctx.si_pipeline(pcm)
+    assert silent.tolist() == [n < 4000 for n in lens]
+    assert np.all(am[silent] == -1)
+    feats = [si_fe.input_feature_gen(p) for p in pcm]
+    x = np.stack([np.zeros((256, 39)) if isinstance(f, str) else f[0] for f in feats]).astype(np.float32)
+    ref = nets.si_forward(x, W, head='sigmoid')
+    ok = ~silent
+    assert np.abs(probs[ok] - ref[ok]).max() <= 1e-4
+    assert np.array_equal(am[ok], ref[ok].argmax(1))
+
+
+def test_device_pointer_mode_matches_host(ctx):
+    import torch
+    from mmla_audio_amd import weights
+    W = weights.synthetic(weights.OD, seed=7)
+    ctx.load_weights(weights.OD, weights.pack(weights.OD, W), 2)
+    pcm = synth.batch(700, 6, 40000)
+    ph, ah = ctx.od_pipeline(pcm)
+    d_pcm = torch.from_numpy(pcm).cuda()
+    d_p = torch.empty((6, 2), dtype=torch.float32, device='cuda')
+    d_a = torch.empty(6, dtype=torch.int32, device='cuda')
+    torch.cuda.synchronize()
+    ctx.od_pipeline_dev(d_pcm.data_ptr(), 6, 40000, 40000, d_p.data_ptr(), d_a.data_ptr())
+    ctx.synchronize()
+    assert np.array_equal(d_p.cpu().numpy(), ph)
+    assert np.array_equal(d_a.cpu().numpy(), ah)
+
+
+def test_no_weights_raises(ctx):
+    from mmla_audio_amd import _lib
+    fresh = _lib.Context(0)
+    with pytest.raises(_lib.MmlaError, match='NOWEIGHTS'):
+        fresh.od_forward(np.zeros((1, 128, 151, 3), np.float32))
