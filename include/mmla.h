@@ -149,6 +149,12 @@ enum mmla_stage {
   MMLA_STAGE_HEAD = 5   /* dense + softmax / sigmoid: work = FLOPs */
 };
 int mmla_profile_enable(mmla_ctx* ctx, int on);
+
+/* Layer-wise parity tap (tests): run OD-NET on host float NHWC x[n,128,151,3] up to `stage`
+ * (0 = stem conv, 1..9 = after res_block 1..9 in NHWC, 10 = mean over H [n,19,128],
+ * 11 = BiLSTM output [n,512]) and copy that tensor to host `out` (capacity out_floats). */
+int mmla_debug_od_trace(mmla_ctx* ctx, const float* x, int64_t n, int stage, float* out,
+                        int64_t out_floats);
 /* ms[MMLA_NSTAGES], launches[MMLA_NSTAGES], work[MMLA_NSTAGES] (each nullable); reset != 0 clears */
 int mmla_profile_read(mmla_ctx* ctx, double* ms, int64_t* launches, double* work, int reset);
 

@@ -48,6 +48,7 @@ SIGNATURES = {
     'mmla_si_pipeline': [_P, _P, _I64, _I64, _P, _I32, _P, _P, _P, _U32],
     'mmla_profile_enable': [_P, ctypes.c_int],
     'mmla_profile_read': [_P, _P, _P, _P, ctypes.c_int],
+    'mmla_debug_od_trace': [_P, _P, _I64, ctypes.c_int, _P, _I64],
 }
 
 NSTAGES = 6
@@ -145,6 +146,19 @@ class Context:
         self._check(self.lib.mmla_profile_read(self.h, _ptr(ms), _ptr(n), _ptr(wk), int(reset)),
                     'mmla_profile_read')
         return {s: (float(ms[i]), int(n[i]), float(wk[i])) for i, s in enumerate(STAGES)}
+
+    def debug_od_trace(self, x, stage):
+        """OD-NET intermediate tensor after `stage` (see mmla.h) for float NHWC input x."""
+        x = np.ascontiguousarray(x, dtype=np.float32)
+        n = x.shape[0]
+        shapes = {0: (128, 151, 16), 10: (19, 128), 11: (512,)}
+        hw = [(64, 76, 32), (64, 76, 32), (64, 76, 32), (32, 38, 64), (32, 38, 64), (32, 38, 64),
+              (16, 19, 128), (16, 19, 128), (16, 19, 128)]
+        shape = shapes.get(stage) or hw[stage - 1]
+        out = np.empty((n,) + shape, np.float32)
+        self._check(self.lib.mmla_debug_od_trace(self.h, _ptr(x), n, int(stage), _ptr(out), out.size),
+                    'mmla_debug_od_trace')
+        return out
 
     def load_weights(self, kind, packed, n_classes, head=HEAD_SOFTMAX):
         packed = np.ascontiguousarray(packed, dtype=np.float32)

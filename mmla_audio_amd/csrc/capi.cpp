@@ -390,8 +390,10 @@ int conv_run(mmla_ctx* c, const ConvArgs& a, int stage = MMLA_STAGE_CONV) {
 double lstm_flops(int64_t n, int T, int D) { return 2.0 * n * T * 2 * (256.0 + D) * 1024.0; }
 
 // OD-NET on a device batch; input = uint8 image (img_u8) or float NHWC (img_f32).
+// `stop` >= 0 (debug trace): return after stage `stop` (0 stem, 1..9 res blocks, 10 mean, 11
+// BiLSTM) with *tap / *tap_n set to that stage's output tensor.
 int run_od_net(mmla_ctx* c, const uint8_t* img_u8, const float* img_f32, int64_t n, float* probs,
-               int32_t* argmax) {
+               int32_t* argmax, int stop = -1, const float** tap = nullptr, int64_t* tap_n = nullptr) {
   const OdNet& W = c->od;
   const size_t big = (size_t)n * OD_PIX * 32 * sizeof(float);
   void *px, *pt1, *pt2, *pseq, *ph;
@@ -405,8 +407,14 @@ int run_od_net(mmla_ctx* c, const uint8_t* img_u8, const float* img_f32, int64_t
   float* T2 = static_cast<float*>(pt2);
   // Conv2D(16, 1x1) on the PNG image (overlap_detector_temp.py:282)
   LAUNCH(c, MMLA_STAGE_GLUE, 2.0 * n * OD_PIX * 3 * 16,
-         od_stem_launch(img_u8, img_f32, n * OD_PIX, W.stem.wt, W.stem.bias, X, c->stream));
+         od_stem_launch(img_u8, img_f32, n * OD_PIX, W.stem.cout_pad, W.stem.wt, W.stem.bias, X,
+                        c->stream));
   int h = OD_H, w = OD_W;
+  if (stop == 0) {
+    *tap = X;
+    *tap_n = n * OD_PIX * 16;
+    return MMLA_OK;
+  }
   for (int b = 0; b < 9; ++b) {   // res_block, overlap_detector_temp.py:253-277
     const OdBlock& B = W.blk[b];
     CHK(conv_run(c, conv_args(B.c3, X, T1, (int)n, h, w, 1, &B.bn_in, PRO_BN_ELU, EPI_BIAS, nullptr)));
@@ -424,13 +432,28 @@ int run_od_net(mmla_ctx* c, const uint8_t* img_u8, const float* img_f32, int64_t
     } else {
       CHK(conv_run(c, conv_args(B.c4, T1, X, (int)n, h, w, 1, &B.bn_mid, PRO_BN_ELU, EPI_ADD, X)));
     }
+    if (stop == b + 1) {
+      *tap = X;
+      *tap_n = n * h * w * CH[b];
+      return MMLA_OK;
+    }
   }
   // h = 16, w = 19, c = 128: Lambda(K.mean(x, axis=1)) -> [n, 19, 128]
   LAUNCH(c, MMLA_STAGE_GLUE, (double)n * h * w * 128,
          mean_h_launch(X, (int)n, h, w, 128, static_cast<float*>(pseq), c->stream));
+  if (stop == 10) {
+    *tap = static_cast<float*>(pseq);
+    *tap_n = n * w * 128;
+    return MMLA_OK;
+  }
   LAUNCH(c, MMLA_STAGE_LSTM, lstm_flops(n, w, 128),
          bilstm_launch(static_cast<float*>(pseq), (int)n, w, 128, W.lstm.wcat[0], W.lstm.wcat[1],
                        W.lstm.bias[0], W.lstm.bias[1], static_cast<float*>(ph), c->stream));
+  if (stop == 11) {
+    *tap = static_cast<float*>(ph);
+    *tap_n = n * 512;
+    return MMLA_OK;
+  }
   LAUNCH(c, MMLA_STAGE_HEAD, 2.0 * n * 512 * 2,
          od_head_launch(static_cast<float*>(ph), (int)n, W.head_w, W.head_b, probs, argmax,
                         c->stream));
@@ -893,6 +916,23 @@ int mmla_si_pipeline(mmla_ctx* c, const int16_t* pcm, int64_t n, int64_t stride,
     if (!dev) HIPCHK(c, hipStreamSynchronize(c->stream));
   }
   return finish(c, dev);
+}
+
+int mmla_debug_od_trace(mmla_ctx* c, const float* x, int64_t n, int stage, float* out,
+                        int64_t out_floats) {
+  if (!c || !x || !out || n < 1 || stage < 0 || stage > 11) return MMLA_E_INVALID;
+  if (!c->od_loaded) return fail(c, MMLA_E_NOWEIGHTS, "OD weights not loaded");
+  HIPCHK(c, hipSetDevice(c->device));
+  void* p = nullptr;
+  CHK(ws_get(c, S_IN, n * OD_IMG * sizeof(float), &p));
+  HIPCHK(c, hipMemcpyAsync(p, x, n * OD_IMG * sizeof(float), hipMemcpyHostToDevice, c->stream));
+  const float* tap = nullptr;
+  int64_t tn = 0;
+  CHK(run_od_net(c, nullptr, static_cast<float*>(p), n, nullptr, nullptr, stage, &tap, &tn));
+  if (tn > out_floats) return fail(c, MMLA_E_SHAPE, "trace stage %d needs %lld floats", stage, (long long)tn);
+  HIPCHK(c, hipMemcpyAsync(out, tap, tn * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return MMLA_OK;
 }
 
 int mmla_profile_enable(mmla_ctx* c, int on) {

@@ -4,7 +4,7 @@
 #include <stdint.h>
 
 // OD stem Conv2D 1x1 3->16 on the decoded PNG (uint8) or a float NHWC input.
-hipError_t od_stem_launch(const uint8_t* img_u8, const float* img_f32, int64_t n_pix,
+hipError_t od_stem_launch(const uint8_t* img_u8, const float* img_f32, int64_t n_pix, int ldw,
                           const float* w /*[3][16]*/, const float* b /*[16]*/, float* y,
                           hipStream_t s);
 // Lambda(K.mean(x, axis=1)): [n, h, w, c] -> [n, w, c]

@@ -14,7 +14,7 @@ namespace {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 template <typename T>
-__global__ void od_stem_kernel(const T* __restrict__ x, int64_t n_pix, const float* __restrict__ w,
+__global__ void od_stem_kernel(const T* __restrict__ x, int64_t n_pix, const float* __restrict__ w, int ldw,
                                const float* __restrict__ b, float* __restrict__ y) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;   // (pixel, output quad)
   if (i >= n_pix * 4) return;
@@ -27,9 +27,9 @@ __global__ void od_stem_kernel(const T* __restrict__ x, int64_t n_pix, const flo
   for (int j = 0; j < 4; ++j) {
     const int co = q * 4 + j;
     // Keras Conv2D 1x1: sum over ci in order, then bias
-    float acc = x0 * w[0 * 16 + co];
-    acc = fmaf(x1, w[1 * 16 + co], acc);
-    acc = fmaf(x2, w[2 * 16 + co], acc);
+    float acc = x0 * w[0 * ldw + co];
+    acc = fmaf(x1, w[1 * ldw + co], acc);
+    acc = fmaf(x2, w[2 * ldw + co], acc);
     op[j] = acc + b[co];
   }
   reinterpret_cast<float4*>(y)[i] = o;
@@ -239,15 +239,15 @@ inline unsigned blocks_for(int64_t work, int bs) { return (unsigned)((work + bs 
 
 }  // namespace
 
-hipError_t od_stem_launch(const uint8_t* img_u8, const float* img_f32, int64_t n_pix,
+hipError_t od_stem_launch(const uint8_t* img_u8, const float* img_f32, int64_t n_pix, int ldw,
                           const float* w, const float* b, float* y, hipStream_t s) {
   if (n_pix <= 0) return hipSuccess;
   if (img_u8)
     hipLaunchKernelGGL(od_stem_kernel<uint8_t>, dim3(blocks_for(n_pix * 4, 256)), dim3(256), 0, s,
-                       img_u8, n_pix, w, b, y);
+                       img_u8, n_pix, w, ldw, b, y);
   else
     hipLaunchKernelGGL(od_stem_kernel<float>, dim3(blocks_for(n_pix * 4, 256)), dim3(256), 0, s,
-                       img_f32, n_pix, w, b, y);
+                       img_f32, n_pix, w, ldw, b, y);
   return hipGetLastError();
 }
 

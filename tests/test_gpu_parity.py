@@ -194,3 +194,44 @@ def test_no_weights_raises(ctx):
     fresh = _lib.Context(0)
     with pytest.raises(_lib.MmlaError, match='NOWEIGHTS'):
         fresh.od_forward(np.zeros((1, 128, 151, 3), np.float32))
+
+
+def _oracle_od_stages(x, W):
+    """Oracle OD-NET intermediate tensors at the mmla_debug_od_trace stages."""
+    x = np.asarray(x, np.float64)
+    out = {}
+    net = nets._conv(x, W, 0)
+    out[0] = net
+    k = 1
+    for b, pool in enumerate(nets.POOL):
+        res = net
+        o = nets._conv(nets.elu(nets.batchnorm(net, W, k)), W, k + 1)
+        o = nets._conv(nets.elu(nets.batchnorm(o, W, k + 2)), W, k + 3)
+        if pool:
+            res = nets._conv(net, W, k + 4, stride=2)
+            o = nets.maxpool2d_same(o)
+            k += 5
+        else:
+            k += 4
+        net = res + o
+        out[b + 1] = net
+    seq = net.mean(axis=1)
+    out[10] = seq
+    out[11] = nets.bilstm(seq, W, 40)
+    return out
+
+
+def test_od_layerwise_trace(ctx):
+    from mmla_audio_amd import weights
+    W = weights.synthetic(weights.OD, seed=8)
+    ctx.load_weights(weights.OD, weights.pack(weights.OD, W), 2)
+    x = np.random.default_rng(9).integers(0, 256, size=(2, 128, 151, 3)).astype(np.float32)
+    ref = _oracle_od_stages(x, W)
+    errs = {}
+    for stage in range(12):
+        got = ctx.debug_od_trace(x, stage)
+        want = ref[stage]
+        assert got.shape == want.shape, (stage, got.shape, want.shape)
+        errs[stage] = float(np.abs(got - want).max() / (np.abs(want).max() + 1e-12))
+    print('relative max-abs error per stage:', errs)
+    assert all(e < 1e-5 for e in errs.values()), errs
