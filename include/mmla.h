@@ -62,6 +62,16 @@ const char* mmla_last_error(const mmla_ctx* ctx);
 /* Use an external hipStream_t (e.g. torch.cuda.current_stream().cuda_stream); NULL = own stream. */
 int mmla_set_stream(mmla_ctx* ctx, void* hip_stream);
 int mmla_synchronize(mmla_ctx* ctx);
+/*
+ * Arithmetic of the spatial convolutions (98 % of OD-NET FLOPs):
+ *   MMLA_PREC_F16X3 (default) error-compensated 3xFP16 on f16 MFMA: operands split hi + 2^-11 lo,
+ *                   hi*hi + hi*lo + lo*hi accumulated in f32 (~22-bit products, f32 accumulation);
+ *                   requires |activations|, |weights| < 65504.
+ *   MMLA_PREC_F32   exact f32 MFMA (v_mfma_f32_32x32x2_f32), 1/5.3 of the throughput.
+ * LSTM, dense heads, 1x1 shortcuts and the front-ends are f32/f64 in both modes.
+ */
+enum mmla_precision { MMLA_PREC_F32 = 0, MMLA_PREC_F16X3 = 1 };
+int mmla_set_precision(mmla_ctx* ctx, int mode);
 /* Cap the clips processed per internal micro-batch (activation memory); 0 = default. */
 int mmla_set_microbatch(mmla_ctx* ctx, int64_t od_clips, int64_t si_clips);
 

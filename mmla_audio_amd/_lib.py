@@ -17,6 +17,7 @@ MMLA_OK = 0
 MMLA_DEVICE_PTR = 0x1
 MODEL_OD, MODEL_SI = 0, 1
 HEAD_SOFTMAX, HEAD_SIGMOID = 0, 1
+PREC_F32, PREC_F16X3 = 0, 1
 
 OD_MELS, OD_FRAMES, OD_CLIP = 128, 151, 24000
 SI_FRAMES, SI_DIMS, SI_SILENT_LEN = 256, 39, 4000
@@ -37,6 +38,7 @@ SIGNATURES = {
     'mmla_set_stream': [_P, _P],
     'mmla_synchronize': [_P],
     'mmla_set_microbatch': [_P, _I64, _I64],
+    'mmla_set_precision': [_P, ctypes.c_int],
     'mmla_load_weights': [_P, ctypes.c_int, _P, _I64, _I32, _I32],
     'mmla_od_features': [_P, _P, _I64, _I64, _P, _I32, _P, _P, _P, _P, _U32],
     'mmla_si_features': [_P, _P, _I64, _I64, _P, _I32, _P, _P, _U32],
@@ -131,6 +133,10 @@ class Context:
 
     def synchronize(self):
         self._check(self.lib.mmla_synchronize(self.h), 'mmla_synchronize')
+
+    def set_precision(self, mode):
+        """PREC_F16X3 (default, 3xFP16 MFMA convs) or PREC_F32 (exact f32 MFMA convs)."""
+        self._check(self.lib.mmla_set_precision(self.h, int(mode)), 'mmla_set_precision')
 
     def set_microbatch(self, od=0, si=0):
         self._check(self.lib.mmla_set_microbatch(self.h, int(od), int(si)), 'mmla_set_microbatch')

@@ -11,6 +11,7 @@
 
 #include "../../include/mmla.h"
 #include "conv.h"
+#include "conv_h3.h"
 #include "nets.h"
 #include "od_fe.h"
 #include "si_fe.h"
@@ -27,7 +28,9 @@ constexpr bool POOL[9] = {true, false, false, true, false, false, true, false, f
 struct ConvW {
   float* wt = nullptr;
   float* bias = nullptr;
-  int kh = 0, kw = 0, cin = 0, cout = 0, cout_pad = 0;
+  uint16_t* wh = nullptr;   // 3xFP16 split weights [tap][cout_pad][cin_pad] (spatial convs only)
+  uint16_t* wl = nullptr;
+  int kh = 0, kw = 0, cin = 0, cout = 0, cout_pad = 0, cin_pad = 0;
 };
 struct BnW {
   float* scale = nullptr;
@@ -90,6 +93,7 @@ struct mmla_ctx {
   std::vector<void*> ws;
   std::vector<size_t> ws_size;
   int64_t od_mb = 4096, si_mb = 16384;
+  int precision = MMLA_PREC_F16X3;
 };
 
 namespace {
@@ -240,6 +244,17 @@ int take_conv(mmla_ctx* c, Cursor& cur, std::vector<void*>& al, int kh, int kw, 
   memcpy(bp.data(), b, sizeof(float) * cout);
   CHK(upload(c, al, kp.data(), kp.size() * sizeof(float), &w->wt));
   CHK(upload(c, al, bp.data(), bp.size() * sizeof(float), &w->bias));
+  if (kh * kw > 1 && cin % 4 == 0) {   // spatial conv: also the 3xFP16 operand layout
+    w->cin_pad = (cin + 15) / 16 * 16;
+    const size_t n = (size_t)kh * kw * w->cout_pad * w->cin_pad;
+    std::vector<uint16_t> hi(n), lo(n);
+    conv_h3_split_weights(k, kh, kw, cin, cout, w->cin_pad, w->cout_pad, hi.data(), lo.data());
+    float* p = nullptr;
+    CHK(upload(c, al, hi.data(), n * sizeof(uint16_t), &p));
+    w->wh = reinterpret_cast<uint16_t*>(p);
+    CHK(upload(c, al, lo.data(), n * sizeof(uint16_t), &p));
+    w->wl = reinterpret_cast<uint16_t*>(p);
+  }
   return MMLA_OK;
 }
 
@@ -387,6 +402,43 @@ int conv_run(mmla_ctx* c, const ConvArgs& a, int stage = MMLA_STAGE_CONV) {
   return MMLA_OK;
 }
 
+// spatial conv on the 3xFP16 path when enabled (falls back to the exact-f32 kernel otherwise);
+// pool_out: write MaxPool2D(2,'same') of the output instead of the output (OD pool blocks).
+int conv_spatial(mmla_ctx* c, const ConvW& w, const float* x, float* y, int n, int h, int wd,
+                 const BnW* bn, int pro, int epi, const float* res, bool pool_out = false) {
+  if (c->precision == MMLA_PREC_F16X3 && w.wh) {
+    ConvH3Args a{};
+    a.x = x;
+    a.wh = w.wh;
+    a.wl = w.wl;
+    a.bias = w.bias;
+    a.scale = bn ? bn->scale : nullptr;
+    a.shift = bn ? bn->shift : nullptr;
+    a.res = res;
+    a.y = y;
+    a.n = n;
+    a.h = h;
+    a.w = wd;
+    a.cin = w.cin;
+    a.cin_pad = w.cin_pad;
+    a.cout = w.cout;
+    a.cout_pad = w.cout_pad;
+    a.kh = w.kh;
+    a.kw = w.kw;
+    a.pad_h = (w.kh - 1) / 2;   // Keras 'same', stride 1: extra padding after
+    a.pad_w = (w.kw - 1) / 2;
+    a.pro = pro;
+    a.epi = epi;
+    a.pool_out = pool_out ? 1 : 0;
+    LAUNCH(c, MMLA_STAGE_CONV, 2.0 * n * h * wd * w.kh * w.kw * w.cin * w.cout,
+           conv_h3_launch(a, c->stream));
+    return MMLA_OK;
+  }
+  ConvArgs a = conv_args(w, x, y, n, h, wd, 1, bn, pro, epi, res);
+  if (!pool_out) return conv_run(c, a);
+  return fail(c, MMLA_E_INVALID, "pooled epilogue needs the 3xFP16 conv path");
+}
+
 double lstm_flops(int64_t n, int T, int D) { return 2.0 * n * T * 2 * (256.0 + D) * 1024.0; }
 
 // OD-NET on a device batch; input = uint8 image (img_u8) or float NHWC (img_f32).
@@ -417,20 +469,27 @@ int run_od_net(mmla_ctx* c, const uint8_t* img_u8, const float* img_f32, int64_t
   }
   for (int b = 0; b < 9; ++b) {   // res_block, overlap_detector_temp.py:253-277
     const OdBlock& B = W.blk[b];
-    CHK(conv_run(c, conv_args(B.c3, X, T1, (int)n, h, w, 1, &B.bn_in, PRO_BN_ELU, EPI_BIAS, nullptr)));
+    CHK(conv_spatial(c, B.c3, X, T1, (int)n, h, w, &B.bn_in, PRO_BN_ELU, EPI_BIAS, nullptr));
     if (POOL[b]) {
-      CHK(conv_run(c, conv_args(B.c4, T1, T2, (int)n, h, w, 1, &B.bn_mid, PRO_BN_ELU, EPI_BIAS,
-                                nullptr)));
-      // shortcut Conv2D(1x1, stride 2) + MaxPool2D(2, 'same')(t2), fused
-      ConvArgs s = conv_args(B.sc, X, T1, (int)n, h, w, 2, nullptr, PRO_NONE, EPI_ADD_POOL, T2);
-      s.hp = h;
-      s.wp = w;
-      CHK(conv_run(c, s));
+      if (c->precision == MMLA_PREC_F16X3) {
+        // conv(4,1) with MaxPool2D(2,'same') fused into its epilogue -> T2 at half resolution;
+        // then shortcut Conv2D(1x1, stride 2) + pooled T2
+        CHK(conv_spatial(c, B.c4, T1, T2, (int)n, h, w, &B.bn_mid, PRO_BN_ELU, EPI_BIAS, nullptr,
+                         true));
+        CHK(conv_run(c, conv_args(B.sc, X, T1, (int)n, h, w, 2, nullptr, PRO_NONE, EPI_ADD, T2)));
+      } else {
+        CHK(conv_spatial(c, B.c4, T1, T2, (int)n, h, w, &B.bn_mid, PRO_BN_ELU, EPI_BIAS, nullptr));
+        // shortcut Conv2D(1x1, stride 2) + MaxPool2D(2, 'same')(t2), fused
+        ConvArgs s = conv_args(B.sc, X, T1, (int)n, h, w, 2, nullptr, PRO_NONE, EPI_ADD_POOL, T2);
+        s.hp = h;
+        s.wp = w;
+        CHK(conv_run(c, s));
+      }
       std::swap(X, T1);
       h = (h + 1) / 2;
       w = (w + 1) / 2;
     } else {
-      CHK(conv_run(c, conv_args(B.c4, T1, X, (int)n, h, w, 1, &B.bn_mid, PRO_BN_ELU, EPI_ADD, X)));
+      CHK(conv_spatial(c, B.c4, T1, X, (int)n, h, w, &B.bn_mid, PRO_BN_ELU, EPI_ADD, X));
     }
     if (stop == b + 1) {
       *tap = X;
@@ -486,16 +545,14 @@ int run_si_net(mmla_ctx* c, const float* x, int64_t n, float* probs, int32_t* ar
       LAUNCH(c, MMLA_STAGE_GLUE, (double)n * t * cin,
              maxpool_t2_launch(X, (int)n, t, cin, XP, c->stream));
       const int tp = (t + 1) / 2;
-      CHK(conv_run(c, conv_args(U.ca, XP, T1, (int)n, tp, 1, 1, &U.bn_in, PRO_BN_RELU, EPI_BIAS,
-                                nullptr)));
+      CHK(conv_spatial(c, U.ca, XP, T1, (int)n, tp, 1, &U.bn_in, PRO_BN_RELU, EPI_BIAS, nullptr));
       CHK(conv_run(c, conv_args(U.sc, X, R, (int)n, t, 1, 2, nullptr, PRO_NONE, EPI_BIAS, nullptr)));
-      CHK(conv_run(c, conv_args(U.cb, T1, R, (int)n, tp, 1, 1, &U.bn_mid, PRO_BN_RELU, EPI_ADD, R)));
+      CHK(conv_spatial(c, U.cb, T1, R, (int)n, tp, 1, &U.bn_mid, PRO_BN_RELU, EPI_ADD, R));
       std::swap(X, R);
       t = tp;
     } else {
-      CHK(conv_run(c, conv_args(U.ca, X, T1, (int)n, t, 1, 1, &U.bn_in, PRO_BN_RELU, EPI_BIAS,
-                                nullptr)));
-      CHK(conv_run(c, conv_args(U.cb, T1, X, (int)n, t, 1, 1, &U.bn_mid, PRO_BN_RELU, EPI_ADD, X)));
+      CHK(conv_spatial(c, U.ca, X, T1, (int)n, t, 1, &U.bn_in, PRO_BN_RELU, EPI_BIAS, nullptr));
+      CHK(conv_spatial(c, U.cb, T1, X, (int)n, t, 1, &U.bn_mid, PRO_BN_RELU, EPI_ADD, X));
     }
   }
   // t = 32, c = 128 -> BN -> ReLU -> AvgPool1D(4) -> [n, 8, 128] (speaker_identification.py:208-212)
@@ -602,6 +659,12 @@ int mmla_set_stream(mmla_ctx* c, void* s) {
 int mmla_synchronize(mmla_ctx* c) {
   if (!c) return MMLA_E_INVALID;
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  return MMLA_OK;
+}
+
+int mmla_set_precision(mmla_ctx* c, int mode) {
+  if (!c || (mode != MMLA_PREC_F32 && mode != MMLA_PREC_F16X3)) return MMLA_E_INVALID;
+  c->precision = mode;
   return MMLA_OK;
 }
 

@@ -1,0 +1,27 @@
+// Halo-tiled implicit-GEMM convolution on gfx950 f16 MFMA with error-compensated 3xFP16 products.
+// See conv_h3.hip.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+struct ConvH3Args {
+  const float* x;        // [N, H, W, Cin] float32 NHWC
+  const uint16_t* wh;    // [KH*KW][CoutPad][CinPad] fp16 hi(w)
+  const uint16_t* wl;    // [KH*KW][CoutPad][CinPad] fp16 lo(w) = fp16((w - hi) * 2^11)
+  const float* bias;     // [CoutPad]
+  const float* scale;    // [Cin] prologue BN scale (nullable when pro == 0)
+  const float* shift;    // [Cin]
+  const float* res;      // EPI_ADD residual [N, H, W, Cout] (may alias y)
+  float* y;              // [N, H, W, Cout]  or pooled [N, ceil(H/2), ceil(W/2), Cout] (pool_out)
+  int n, h, w, cin, cin_pad, cout, cout_pad;
+  int kh, kw, pad_h, pad_w;
+  int th, tw;            // output tile (th * tw <= 128)
+  int tiles_h, tiles_w;
+  int pro, epi, pool_out;
+};
+
+// Picks the tile and launches; returns hipErrorInvalidValue for unsupported shapes.
+hipError_t conv_h3_launch(ConvH3Args a, hipStream_t stream);
+// Host: split float32 weights [kh,kw,cin,cout] into the fp16 hi/lo [tap][cout_pad][cin_pad] layout.
+void conv_h3_split_weights(const float* w, int kh, int kw, int cin, int cout, int cin_pad,
+                           int cout_pad, uint16_t* hi, uint16_t* lo);

@@ -235,3 +235,29 @@ def test_od_layerwise_trace(ctx):
         errs[stage] = float(np.abs(got - want).max() / (np.abs(want).max() + 1e-12))
     print('relative max-abs error per stage:', errs)
     assert all(e < 1e-5 for e in errs.values()), errs
+
+
+@pytest.mark.parametrize('prec', [0, 1])
+def test_precision_modes_vs_oracle(ctx, prec, si_golden):
+    """Both conv arithmetics (exact f32 MFMA, 3xFP16 MFMA) hold the 1e-4 probability bar."""
+    from mmla_audio_amd import _lib, weights
+    ctx.set_precision(prec)
+    try:
+        W = weights.synthetic(weights.OD, seed=11)
+        ctx.load_weights(weights.OD, weights.pack(weights.OD, W), 2)
+        x = np.random.default_rng(12).integers(0, 256, size=(6, 128, 151, 3)).astype(np.float32)
+        p = ctx.od_forward(x)
+        ref = nets.od_forward(x, W)
+        assert np.abs(p - ref).max() <= 1e-4, (prec, np.abs(p - ref).max())
+        for stage in (1, 4, 9, 11):
+            got = ctx.debug_od_trace(x[:2], stage)
+            want = _oracle_od_stages(x[:2], W)[stage]
+            rel = np.abs(got - want).max() / np.abs(want).max()
+            assert rel < 1e-5, (prec, stage, rel)
+        Ws = weights.synthetic(weights.SI, seed=13, n_classes=630)
+        ctx.load_weights(weights.SI, weights.pack(weights.SI, Ws, 630), 630, 0)
+        xs = np.stack([si_golden[f'feat_{i}'][0] for i in range(len(si_golden['names']))]).astype(np.float32)
+        ps = ctx.si_forward(xs)
+        assert np.abs(ps - nets.si_forward(xs, Ws)).max() <= 1e-4
+    finally:
+        ctx.set_precision(_lib.PREC_F16X3)
