@@ -7,18 +7,20 @@
 //     y     = acc1 + 2^-11 acc2                 (dropped term lo*lo*2^-22 <= 2^-22 |a w|)
 // i.e. ~22-bit products with float32 accumulation -- float32-class accuracy (the reference's Keras
 // layers run float32) at 16/3 = 5.3x the f32-MFMA rate.  Layer-wise parity vs the float64 oracle:
-// tests/test_gpu_parity.py::test_od_layerwise_trace.
+// tests/test_gpu_parity.py::test_od_layerwise_trace / test_precision_modes_vs_oracle.
 //
-// Tiling (256 threads = 4 waves): one workgroup computes a TH x TW (<= 128 pixel) output tile of one
-// clip for BN output channels.  Per chunk of CK input channels the (TH+KH-1) x (TW+KW-1) input halo
-// is staged ONCE into LDS -- with the BatchNorm + ELU/ReLU prologue applied once per input element
-// (not once per tap) and split into fp16 hi/lo -- and all KH*KW taps read their A fragments from
-// it (ds_read_b128, pixel rows padded by 16 B: conflict-free).  B fragments (pre-split weights,
-// [tap][cout][cin] so a lane's 8 k-values are one 16-B load) come from L2 with the next tap's
-// prefetched under the current tap's MFMAs.  Waves split the tile 4x1 (BN = 32) or 2x2 (BN >= 64).
-// Epilogue: bias, optional in-place residual, or (pool blocks) MaxPool2D(2,'same') of the tile
-// written at half resolution -- the 2x2 window lives in one lane's accumulator registers when
-// TW = 16 (rows r, r+1, r+16, r+17 of a 32-row MFMA tile).
+// One workgroup (256 threads = 4 waves) computes a TH x TW = 128-pixel output tile of one clip for
+// BN output channels; TW is a compile-time 16 (wide images), 8 (narrow) or 1 (the SI Conv1D), so
+// every pixel <-> (row, col) map is a shift.  Per chunk of CK input channels the
+// (TH+KH-1) x (TW+KW-1) input halo is staged ONCE into LDS -- BatchNorm + ELU/ReLU prologue applied
+// once per input element (not once per tap), split into fp16 hi/lo -- and all KH*KW taps read their
+// A fragments from it (ds_read_b128, pixel rows padded by 16 B).  B fragments (pre-split weights
+// [tap][cout][cin]: a lane's 8 k-values are one 16-B load) come from L2, next tap prefetched under
+// the current tap's MFMAs.  Waves split the tile 4 x 1 / 2 x 2 / 1 x 4 (BN = 32 / 64 / 128): every
+// wave owns its own 32 output channels, so no B fragment is fetched twice per workgroup.
+// Epilogue: bias, optional in-place residual, or (pool blocks) MaxPool2D(2,'same') written at half
+// resolution: the 2x2 window is rows r, r+1, r+TW, r+TW+1 of one lane's 32-row accumulator tile,
+// so no data leaves the registers.
 #include "common.h"
 #include "conv.h"
 #include "conv_h3.h"
@@ -42,42 +44,46 @@ MMLA_DEV float pro_fn(float v, float sc, float sh) {
     return v;
   } else {
     v = fmaf(v, sc, sh);
-    if constexpr (PRO == PRO_BN_ELU) return v > 0.0f ? v : expm1f(v);
+    // Keras/TF Elu: exp(x) - 1 for x < 0 (Eigen: (x < 0).select(x.exp() - 1, x))
+    if constexpr (PRO == PRO_BN_ELU) return v > 0.0f ? v : __expf(v) - 1.0f;
     return fmaxf(v, 0.0f);
   }
 }
 
-template <int KH, int KW, int CK, int BN, int PRO, int EPI, bool POOL>
-__global__ void __launch_bounds__(NT, BN >= 128 ? 1 : 2) conv_h3_kernel(ConvH3Args a) {
-  constexpr int WN = BN >= 64 ? 2 : 1;
+template <int KH, int KW, int CK, int BN, int TW, int PRO, int EPI, bool POOL>
+__global__ void __launch_bounds__(NT, 2) conv_h3_kernel(ConvH3Args a) {
+  // each wave owns ONE 32-column slice of B (no B fragment is loaded by two waves) and
+  // 128 / WM rows: BN 32 -> 4 x 1, BN 64 -> 2 x 2, BN 128 -> 1 x 4 (waves along N)
+  constexpr int WN = BN / 32;
   constexpr int WM = 4 / WN;
   constexpr int MT = BM / (WM * 32);      // 32-row tiles per wave
   constexpr int NTL = BN / (WN * 32);     // 32-col tiles per wave
-  constexpr int LDP = CK + 8;             // fp16 per staged pixel (16-B pad: conflict-free b128)
+  constexpr int LDP = CK + 8;             // fp16 per staged pixel (16-B pad)
   constexpr int KS = CK / 16;             // MFMA k-steps per chunk
   constexpr int TAPS = KH * KW;
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int WP = a.tw + KW - 1;
-  const int npix = (a.th + KH - 1) * WP;
-  _Float16* lds_hi = reinterpret_cast<_Float16*>(smem);
-  _Float16* lds_lo = lds_hi + npix * LDP;
+  constexpr int TH = BM / TW;
+  constexpr int WP = TW + KW - 1;
+  constexpr int HP = TH + KH - 1;
+  constexpr int NPIX = HP * WP;
+  constexpr int QPP = CK / 4;             // float4 per staged pixel
+  __shared__ __attribute__((aligned(16))) _Float16 lds_hi[NPIX * LDP];
+  __shared__ __attribute__((aligned(16))) _Float16 lds_lo[NPIX * LDP];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave - (wave / WN) * WN;
   const int tiles = a.tiles_h * a.tiles_w;
   const int64_t clip = blockIdx.x / tiles;
   const int tile = blockIdx.x - (int)(clip * tiles);
-  const int h0 = (tile / a.tiles_w) * a.th;
-  const int w0 = (tile - (tile / a.tiles_w) * a.tiles_w) * a.tw;
+  const int th_i = tile / a.tiles_w;
+  const int h0 = th_i * TH;
+  const int w0 = (tile - th_i * a.tiles_w) * TW;
   const int n0 = blockIdx.y * BN;
-  const int tpix = a.th * a.tw;
 
   int apix[MT];
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
     const int m = (wm * MT + mt) * 32 + (lane & 31);
-    const int th = m / a.tw, tw = m - (m / a.tw) * a.tw;
-    apix[mt] = m < tpix ? (th * WP + tw) * LDP : 0;
+    apix[mt] = ((m / TW) * WP + (m % TW)) * LDP;
   }
   const int koff = (lane >> 5) * 8;
 
@@ -101,21 +107,42 @@ __global__ void __launch_bounds__(NT, BN >= 128 ? 1 : 2) conv_h3_kernel(ConvH3Ar
     wlp[nt] = a.wl + (size_t)co * a.cin_pad + koff;
   }
   const size_t tap_stride = (size_t)a.cout_pad * a.cin_pad;
+  const float* xclip = a.x + clip * a.h * a.w * a.cin;
 
   const int nchunks = a.cin_pad / CK;
   for (int ch = 0; ch < nchunks; ++ch) {
     const int ci0 = ch * CK;
     __syncthreads();   // every wave is done reading the previous chunk's halo
     // ---- stage the input halo of this channel chunk: prologue once per element, split hi/lo ----
-    for (int task = tid; task < npix * (CK / 4); task += NT) {
-      const int px = task / (CK / 4), q = task - px * (CK / 4);
-      const int py = px / WP, pxx = px - py * WP;
-      const int ih = h0 - a.pad_h + py, iw = w0 - a.pad_w + pxx;
+    // all of this thread's halo loads are issued before the first is consumed (one HBM latency
+    // per chunk, not one per element group)
+    constexpr int MAXT = (NPIX * QPP + NT - 1) / NT;
+    float4 pre[MAXT];
+    uint32_t valid = 0;
+#pragma unroll
+    for (int j = 0; j < MAXT; ++j) {
+      const int task = tid + j * NT;
+      pre[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (task < NPIX * QPP) {
+        const int px = task / QPP, q = task % QPP;
+        const int py = px / WP, pxx = px % WP;
+        const int ih = h0 - a.pad_h + py, iw = w0 - a.pad_w + pxx;
+        const int ci = ci0 + q * 4;
+        if (ih >= 0 && ih < a.h && iw >= 0 && iw < a.w && ci < a.cin) {
+          pre[j] = *reinterpret_cast<const float4*>(xclip + (ih * a.w + iw) * a.cin + ci);
+          valid |= 1u << j;
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < MAXT; ++j) {
+      const int task = tid + j * NT;
+      if (task >= NPIX * QPP) continue;
+      const int px = task / QPP, q = task % QPP;
       const int ci = ci0 + q * 4;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (ih >= 0 && ih < a.h && iw >= 0 && iw < a.w && ci < a.cin) {
-        v = *reinterpret_cast<const float4*>(a.x + ((clip * a.h + ih) * a.w + iw) * a.cin + ci);
-        if constexpr (PRO != PRO_NONE) {
+      float4 v = pre[j];
+      if constexpr (PRO != PRO_NONE) {
+        if (valid & (1u << j)) {
           const float4 sc = *reinterpret_cast<const float4*>(a.scale + ci);
           const float4 sh = *reinterpret_cast<const float4*>(a.shift + ci);
           v.x = pro_fn<PRO>(v.x, sc.x, sh.x);
@@ -149,7 +176,9 @@ __global__ void __launch_bounds__(NT, BN >= 128 ? 1 : 2) conv_h3_kernel(ConvH3Ar
       }
 #pragma unroll
     for (int tap = 0; tap < TAPS; ++tap) {
-      const int dy = tap / KW, dx = tap - (tap / KW) * KW;
+      constexpr int dummy = 0;
+      (void)dummy;
+      const int dy = tap / KW, dx = tap % KW;
       const int toff = (dy * WP + dx) * LDP;
       f16x8 nbh[NTL][KS], nbl[NTL][KS];
       if (tap + 1 < TAPS) {   // prefetch the next tap's B fragments under this tap's MFMAs
@@ -188,7 +217,9 @@ __global__ void __launch_bounds__(NT, BN >= 128 ? 1 : 2) conv_h3_kernel(ConvH3Ar
     }
   }
 
-  // ---- epilogue --------------------------------------------------------------------------------
+  // ---- epilogue ----------------------------------------------------------------------------------
+  // lane's accumulator register r holds tile row m = mbase + (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
+  const int hsel = 4 * (lane >> 5);
 #pragma unroll
   for (int nt = 0; nt < NTL; ++nt) {
     const int co = n0 + (wn * NTL + nt) * 32 + (lane & 31);
@@ -201,91 +232,67 @@ __global__ void __launch_bounds__(NT, BN >= 128 ? 1 : 2) conv_h3_kernel(ConvH3Ar
       for (int r = 0; r < 16; ++r) v[r] = acc1[mt][nt][r] + acc2[mt][nt][r] * LO_INV + b;
       const int mbase = (wm * MT + mt) * 32;
       if constexpr (POOL) {
-        // TW == 16: this 32-row tile holds output rows (th, th+1), th = mbase / 16 (even)
-        const int oh = h0 + mbase / 16;
-        const int hp = (a.h + 1) / 2, wp = (a.w + 1) / 2;
-        if (mbase < tpix && oh < a.h) {
+        // windows: top-left rows i = 8q + hsel + e (i % TW even, (i / TW) even) -> registers
+        // {4q+e, 4q+e+1, 4q+e+TW/2, 4q+e+TW/2+1}  (row + TW = register + TW/2)
+        static_assert(TW == 16 || TW == 8, "pooled epilogue needs TW 8 or 16");
+        const int hp = (a.h + 1) >> 1, wp = (a.w + 1) >> 1;
 #pragma unroll
-          for (int q = 0; q < 2; ++q)
+        for (int q = 0; q < 4; ++q)
 #pragma unroll
-            for (int e = 0; e < 4; e += 2) {
-              const int twi = 8 * q + 4 * (lane >> 5) + e;   // even column of the window
-              const int ow = w0 + twi;
-              if (ow >= a.w) continue;
-              float mx = v[4 * q + e];
-              if (ow + 1 < a.w) mx = fmaxf(mx, v[4 * q + e + 1]);
-              if (oh + 1 < a.h) {
-                mx = fmaxf(mx, v[4 * q + 8 + e]);
-                if (ow + 1 < a.w) mx = fmaxf(mx, v[4 * q + 9 + e]);
-              }
-              a.y[((clip * hp + oh / 2) * wp + ow / 2) * a.cout + co] = mx;
+          for (int e = 0; e < 4; e += 2) {
+            constexpr int R = TW / 2;
+            const int i = 8 * q + hsel + e;
+            if ((i / TW) & 1) continue;                    // only top rows of window pairs
+            if (4 * q + e + R + 1 > 15) continue;
+            const int m = mbase + i;
+            const int oh = h0 + m / TW, ow = w0 + m % TW;
+            if (oh >= a.h || ow >= a.w) continue;
+            float mx = v[4 * q + e];
+            if (ow + 1 < a.w) mx = fmaxf(mx, v[4 * q + e + 1]);
+            if (oh + 1 < a.h) {
+              mx = fmaxf(mx, v[4 * q + e + R]);
+              if (ow + 1 < a.w) mx = fmaxf(mx, v[4 * q + e + R + 1]);
             }
-        }
+            a.y[((clip * hp + (oh >> 1)) * wp + (ow >> 1)) * a.cout + co] = mx;
+          }
       } else {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int m = mbase + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-          if (m >= tpix) continue;
-          const int oh = h0 + m / a.tw, ow = w0 + (m - (m / a.tw) * a.tw);
-          if (oh >= a.h || ow >= a.w) continue;
-          const int64_t p = (clip * a.h + oh) * a.w + ow;
-          float val = v[r];
-          if constexpr (EPI == EPI_ADD) val += a.res[p * a.cout + co];
-          a.y[p * a.cout + co] = val;
+        for (int g = 0; g < 4; ++g) {        // 4 groups of 4 consecutive tile rows
+          const int m0 = mbase + 8 * g + hsel;
+          const int oh = h0 + m0 / TW;
+          if (oh >= a.h) continue;
+          const int ow0 = w0 + m0 % TW;
+          float* yp = a.y + ((clip * a.h + oh) * a.w + ow0) * a.cout + co;
+          const float* rp = nullptr;
+          if constexpr (EPI == EPI_ADD) rp = a.res + ((clip * a.h + oh) * a.w + ow0) * a.cout + co;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            // TW >= 4 keeps the 4 rows in one image row; TW == 1 walks image rows instead
+            const int step = TW == 1 ? a.w * a.cout : a.cout;
+            const bool ok = TW == 1 ? (oh + j < a.h) : (ow0 + j < a.w);
+            if (!ok) continue;
+            float val = v[4 * g + j];
+            if constexpr (EPI == EPI_ADD) val += rp[j * step];
+            yp[j * step] = val;
+          }
         }
       }
     }
   }
 }
 
-template <int KH, int KW, int CK, int BN, int PRO, int EPI, bool POOL>
+template <int KH, int KW, int CK, int BN, int TW, int PRO, int EPI, bool POOL>
 hipError_t launch(const ConvH3Args& a, hipStream_t s) {
-  const size_t smem = (size_t)(a.th + KH - 1) * (a.tw + KW - 1) * (CK + 8) * 2 * sizeof(_Float16);
-  auto k = conv_h3_kernel<KH, KW, CK, BN, PRO, EPI, POOL>;
-  if (smem > 64 * 1024) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-    if (e != hipSuccess) return e;
-  }
   dim3 grid((unsigned)((int64_t)a.n * a.tiles_h * a.tiles_w), (unsigned)(a.cout_pad / BN));
-  hipLaunchKernelGGL(k, grid, dim3(NT), smem, s, a);
+  hipLaunchKernelGGL((conv_h3_kernel<KH, KW, CK, BN, TW, PRO, EPI, POOL>), grid, dim3(NT), 0, s, a);
   return hipGetLastError();
 }
 
-template <int KH, int KW, int CK, int PRO, int EPI, bool POOL>
+template <int KH, int KW, int CK, int TW, int PRO, int EPI, bool POOL>
 hipError_t by_bn(const ConvH3Args& a, hipStream_t s) {
-  if (a.cout_pad % 128 == 0) return launch<KH, KW, CK, 128, PRO, EPI, POOL>(a, s);
-  if (a.cout_pad % 64 == 0) return launch<KH, KW, CK, 64, PRO, EPI, POOL>(a, s);
-  return launch<KH, KW, CK, 32, PRO, EPI, POOL>(a, s);
-}
-
-// pick (th, tw): minimise MFMA rows issued + halo staging over the whole image
-void pick_tile(ConvH3Args& a) {
-  if (a.pool_out) {   // the fused 2x2 pool needs TW = 16, TH = 8 (aligned, even)
-    a.tw = 16;
-    a.th = 8;
-  } else if (a.w == 1) {
-    a.tw = 1;
-    a.th = 128;
-  } else {
-    double best = 1e30;
-    const int cands[] = {8, 16, 19, 20, 32, 38, 40, 64, 76};
-    for (int tw : cands) {
-      if (tw > 2 * a.w && tw != 8) continue;
-      const int th = BM / tw;
-      if (th < 1) continue;
-      const int tiles = ((a.h + th - 1) / th) * ((a.w + tw - 1) / tw);
-      const double halo = (double)(th + a.kh - 1) * (tw + a.kw - 1);
-      const double cost = tiles * (BM * a.kh * a.kw * 1.0 + halo * 2.0);
-      if (cost < best) {
-        best = cost;
-        a.tw = tw;
-        a.th = th;
-      }
-    }
-  }
-  a.tiles_h = (a.h + a.th - 1) / a.th;
-  a.tiles_w = (a.w + a.tw - 1) / a.tw;
+  if (a.cout_pad % 128 == 0) return launch<KH, KW, CK, 128, TW, PRO, EPI, POOL>(a, s);
+  if (a.cout_pad % 64 == 0) return launch<KH, KW, CK, 64, TW, PRO, EPI, POOL>(a, s);
+  return launch<KH, KW, CK, 32, TW, PRO, EPI, POOL>(a, s);
 }
 
 }  // namespace
@@ -293,20 +300,28 @@ void pick_tile(ConvH3Args& a) {
 hipError_t conv_h3_launch(ConvH3Args a, hipStream_t s) {
   if ((int64_t)a.n * a.h * a.w == 0) return hipSuccess;
   if (a.cin % 4 != 0 || a.cout_pad % 32 != 0) return hipErrorInvalidValue;
-  pick_tile(a);
+  // tile: 16 wide for wide images, 8 for narrow ones (W = 38, 19), 1 for Conv1D
+  a.tw = a.w == 1 ? 1 : (a.w >= 48 ? 16 : 8);
+  a.th = BM / a.tw;
+  a.tiles_h = (a.h + a.th - 1) / a.th;
+  a.tiles_w = (a.w + a.tw - 1) / a.tw;
   const int ck = a.cin_pad % 32 == 0 ? 32 : 16;
   if (a.cin_pad % ck != 0) return hipErrorInvalidValue;
-#define H3(KH, KW, CK, P, E, PL)                                                            \
-  if (a.kh == KH && a.kw == KW && ck == CK && a.pro == P && a.epi == E && (a.pool_out != 0) == PL) \
-    return by_bn<KH, KW, CK, P, E, PL>(a, s);
+#define H3(KH, KW, CK, TW, P, E, PL)                                                           \
+  if (a.kh == KH && a.kw == KW && ck == CK && a.tw == TW && a.pro == P && a.epi == E &&        \
+      (a.pool_out != 0) == PL)                                                                 \
+    return by_bn<KH, KW, CK, TW, P, E, PL>(a, s);
   // OD-NET res_block convs (overlap_detector_temp.py:258-274)
-  H3(3, 3, 16, PRO_BN_ELU, EPI_BIAS, false)
-  H3(3, 3, 32, PRO_BN_ELU, EPI_BIAS, false)
-  H3(4, 1, 32, PRO_BN_ELU, EPI_BIAS, true)
-  H3(4, 1, 32, PRO_BN_ELU, EPI_ADD, false)
+  H3(3, 3, 16, 16, PRO_BN_ELU, EPI_BIAS, false)
+  H3(3, 3, 32, 16, PRO_BN_ELU, EPI_BIAS, false)
+  H3(3, 3, 32, 8, PRO_BN_ELU, EPI_BIAS, false)
+  H3(4, 1, 32, 16, PRO_BN_ELU, EPI_BIAS, true)
+  H3(4, 1, 32, 8, PRO_BN_ELU, EPI_BIAS, true)
+  H3(4, 1, 32, 16, PRO_BN_ELU, EPI_ADD, false)
+  H3(4, 1, 32, 8, PRO_BN_ELU, EPI_ADD, false)
   // SI-NET res_unit convs (speaker_identification.py:173-188)
-  H3(3, 1, 32, PRO_BN_RELU, EPI_BIAS, false)
-  H3(3, 1, 32, PRO_BN_RELU, EPI_ADD, false)
+  H3(3, 1, 32, 1, PRO_BN_RELU, EPI_BIAS, false)
+  H3(3, 1, 32, 1, PRO_BN_RELU, EPI_ADD, false)
 #undef H3
   return hipErrorInvalidValue;
 }
