@@ -27,6 +27,9 @@ sys.path.insert(0, REPO)
 METRIC = 'audio clips/sec (MFCC→logits) at 1/2/4/8 MI355X; MFCC max-abs-err vs librosa'
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md chip table (spec)
 F32_MFMA_PEAK_TFS = 157.3    # v_mfma_f32_32x32x2_f32, dense
+F16_MFMA_PEAK_TFS = 2516.6   # f16 MFMA dense (~2.5 PF spec, no sparsity)
+# 3xFP16 spends three f16 MFMA products per f32 MAC: its f32-equivalent ceiling is F16 / 3
+F16X3_PEAK_TFS = F16_MFMA_PEAK_TFS / 3
 OD_FE_BYTES = 48000 + 128 * 151 * 4 + 151 * 4          # 125 916 B/clip
 
 
@@ -195,8 +198,10 @@ def main():
                 'frac': achieved / HBM_PEAK_GBS, 'traffic': None}
     else:
         achieved = work / (ms * 1e-3) / 1e12
-        roof = {'bound': 'mfma', 'achieved': achieved, 'peak': F32_MFMA_PEAK_TFS, 'unit': 'TFLOP/s',
-                'frac': achieved / F32_MFMA_PEAK_TFS, 'traffic': None}
+        peak = F16X3_PEAK_TFS if stage == 'conv' else F32_MFMA_PEAK_TFS
+        roof = {'bound': 'mfma', 'achieved': achieved, 'peak': peak, 'unit': 'TFLOP/s',
+                'frac': achieved / peak, 'traffic': None,
+                'arith': '3xFP16 on f16 MFMA (peak = f16 dense / 3)' if stage == 'conv' else 'f32 MFMA'}
     roof.update({'kernel': stage, 'launches': launches, 'avg_launch_ms': ms / max(launches, 1),
                  'work_per_launch': work / max(launches, 1)})
     stages = {s: {'ms': round(v[0], 3), 'launches': v[1],

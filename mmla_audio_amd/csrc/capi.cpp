@@ -13,6 +13,7 @@
 #include "conv.h"
 #include "conv_h3.h"
 #include "nets.h"
+#include "resblk.h"
 #include "od_fe.h"
 #include "si_fe.h"
 
@@ -30,7 +31,9 @@ struct ConvW {
   float* bias = nullptr;
   uint16_t* wh = nullptr;   // 3xFP16 split weights [tap][cout_pad][cin_pad] (spatial convs only)
   uint16_t* wl = nullptr;
-  int kh = 0, kw = 0, cin = 0, cout = 0, cout_pad = 0, cin_pad = 0;
+  uint16_t* fh = nullptr;   // fused res_block layout [cout][kpad], k = tap * cin + ci (resblk.hip)
+  uint16_t* fl = nullptr;
+  int kh = 0, kw = 0, cin = 0, cout = 0, cout_pad = 0, cin_pad = 0, kpad = 0;
 };
 struct BnW {
   float* scale = nullptr;
@@ -255,6 +258,17 @@ int take_conv(mmla_ctx* c, Cursor& cur, std::vector<void*>& al, int kh, int kw, 
     CHK(upload(c, al, lo.data(), n * sizeof(uint16_t), &p));
     w->wl = reinterpret_cast<uint16_t*>(p);
   }
+  if (kh * kw > 1 && cin % 16 == 0 && cout % 16 == 0) {
+    w->kpad = (kh * kw * cin + 31) / 32 * 32;
+    const size_t n = (size_t)cout * w->kpad;
+    std::vector<uint16_t> hi(n), lo(n);
+    resblk_split_weights(k, kh * kw, cin, cout, w->kpad, hi.data(), lo.data());
+    float* p = nullptr;
+    CHK(upload(c, al, hi.data(), n * sizeof(uint16_t), &p));
+    w->fh = reinterpret_cast<uint16_t*>(p);
+    CHK(upload(c, al, lo.data(), n * sizeof(uint16_t), &p));
+    w->fl = reinterpret_cast<uint16_t*>(p);
+  }
   return MMLA_OK;
 }
 
@@ -469,6 +483,41 @@ int run_od_net(mmla_ctx* c, const uint8_t* img_u8, const float* img_f32, int64_t
   }
   for (int b = 0; b < 9; ++b) {   // res_block, overlap_detector_temp.py:253-277
     const OdBlock& B = W.blk[b];
+    if (c->precision == MMLA_PREC_F16X3 && B.c3.fh && B.c4.fh && B.c4.kpad == 4 * B.c4.cin &&
+        resblk_supported(B.c3.cin, B.c3.cout, POOL[b])) {
+      // whole block in one launch: t1 stays in LDS (resblk.hip)
+      ResBlkArgs r{};
+      r.x = X;
+      r.w1h = B.c3.fh;
+      r.w1l = B.c3.fl;
+      r.b1 = B.c3.bias;
+      r.s1 = B.bn_in.scale;
+      r.t1 = B.bn_in.shift;
+      r.w2h = B.c4.fh;
+      r.w2l = B.c4.fl;
+      r.b2 = B.c4.bias;
+      r.s2 = B.bn_mid.scale;
+      r.t2 = B.bn_mid.shift;
+      r.y = POOL[b] ? T2 : T1;
+      r.n = (int)n;
+      r.h = h;
+      r.w = w;
+      LAUNCH(c, MMLA_STAGE_CONV,
+             2.0 * n * h * w * (9.0 * B.c3.cin * B.c3.cout + 4.0 * B.c4.cin * B.c4.cout),
+             resblk_launch(r, B.c3.cin, B.c3.cout, POOL[b], c->stream));
+      if (POOL[b]) {   // + Conv2D(1x1, stride 2)(x)
+        CHK(conv_run(c, conv_args(B.sc, X, T1, (int)n, h, w, 2, nullptr, PRO_NONE, EPI_ADD, T2)));
+        h = (h + 1) / 2;
+        w = (w + 1) / 2;
+      }
+      std::swap(X, T1);
+      if (stop == b + 1) {
+        *tap = X;
+        *tap_n = n * h * w * CH[b];
+        return MMLA_OK;
+      }
+      continue;
+    }
     CHK(conv_spatial(c, B.c3, X, T1, (int)n, h, w, &B.bn_in, PRO_BN_ELU, EPI_BIAS, nullptr));
     if (POOL[b]) {
       if (c->precision == MMLA_PREC_F16X3) {

@@ -1,0 +1,31 @@
+// One fused OD-NET res_block on gfx950 f16 MFMA (3xFP16).  See resblk.hip.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+struct ResBlkArgs {
+  const float* x;          // [N, H, W, CIN] block input (raw: also the residual of non-pool blocks)
+  const uint16_t* w1h;     // Conv2D(3x3) fp16 hi [C][K1PAD], k = (dy * 3 + dx) * CIN + ci
+  const uint16_t* w1l;     //                 lo = fp16((w - hi) * 2^11)
+  const float* b1;         // [C]
+  const float* s1;         // BatchNorm before the 3x3 conv, folded: y = x * s1 + t1   [CIN]
+  const float* t1;
+  const uint16_t* w2h;     // Conv2D((4,1)) fp16 hi [C][4 * C], k = dy * C + ci
+  const uint16_t* w2l;
+  const float* b2;         // [C]
+  const float* s2;         // BatchNorm before the (4,1) conv, folded [C]
+  const float* t2;
+  float* y;                // non-pool: [N, H, W, C] = x + conv;  pool: [N, ceil(H/2), ceil(W/2), C]
+  int n, h, w;             // = MaxPool2D(2, 'same')(conv)   (the 1x1/2 shortcut is added after)
+  int tiles_h, tiles_w;    // set by resblk_launch
+};
+
+// K of the 3x3 conv padded to the MFMA k-step (32).
+int resblk_k1pad(int cin);
+// True when (cin, c, pool) has a fused kernel.
+bool resblk_supported(int cin, int c, bool pool);
+hipError_t resblk_launch(ResBlkArgs a, int cin, int c, bool pool, hipStream_t stream);
+// Host: float32 Keras weights [taps][cin][cout] -> fp16 hi/lo [cout][kpad] with k = tap * cin + ci
+// (zero for k >= taps * cin).
+void resblk_split_weights(const float* w, int taps, int cin, int cout, int kpad, uint16_t* hi,
+                          uint16_t* lo);

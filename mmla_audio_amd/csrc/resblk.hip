@@ -1,0 +1,424 @@
+// Fused OD-NET res_block (overlap_detector_temp.py:253-277) on gfx950 f16 MFMA, 3xFP16 products.
+//
+//   t1 = Conv2D(C, 3x3, same)(ELU(BN1(x)))              -- GEMM 1, K = 9 * CIN
+//   t2 = Conv2D(C, (4,1), same)(ELU(BN2(t1)))           -- GEMM 2, K = 4 * C
+//   y  = x + t2                       (non-pool blocks)
+//   y  = MaxPool2D(2, same)(t2)       (pool blocks; the Conv2D(1x1, stride 2) shortcut is added by
+//                                      the next launch, conv.hip EPI_ADD)
+//
+// One workgroup (4 waves) owns a 16 x 16 output tile of one clip and ALL C channels.  The
+// intermediate t1 never touches HBM: its 19 x 16 tile (one row above, two below: the (4,1) 'same'
+// padding) is computed from a 21 x 18 input halo staged in LDS, BN2 + ELU + the hi/lo split are applied
+// once per element, and the result is re-staged in the SAME LDS bytes for GEMM 2.  HBM traffic per
+// block is the input halo (21*18 / 16*16 = 1.48 x the input) plus the output, instead of
+// in + t1 + t1 + out (+ residual) for the two-launch form; the price is recomputing 3 of every 19 t1
+// rows.
+//
+// MFMA v_mfma_f32_16x16x32_f16: one 16-row M tile = one 16-pixel image row segment of the tile, so
+// the pixel <-> (row, col) map is the tile row index and the lane's column.  Lane l holds
+// A[row l & 15][k 8 (l >> 4) .. +7] (one ds_read_b128 per operand half), B[k 8 (l >> 4) .. +7][col
+// l & 15] (one 16-B global load from the [C][K] weight image) and C[rows 4 (l >> 4) .. +3][col l & 15].
+// K runs over (tap, channel) with the channel fastest, so CIN = 16 packs two taps per k-step.
+// 3xFP16: acc1 += hi*hi, acc2 += hi*lo + lo*hi; value = acc1 + 2^-11 acc2 (see conv_h3.hip).
+#include "resblk.h"
+
+#ifndef RB_EXP
+#define RB_EXP 0   // experiment switch for profiling (0 = product)
+#endif
+
+#include <algorithm>
+#include <cstring>
+
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+
+constexpr int NT = 256;
+constexpr int TW = 16;
+constexpr int TH = 16;
+constexpr float LO_SCALE = 2048.0f;
+constexpr float LO_INV = 1.0f / 2048.0f;
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+constexpr float LOG2E = 1.4426950408889634f;
+
+// TF Elu on a pair (v_pk_* for the arithmetic): x > 0 ? x : exp(x) - 1
+__device__ __forceinline__ f32x2 elu2(f32x2 u) {
+  const f32x2 t = u * LOG2E;
+  f32x2 e = {__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)};
+  e = e - 1.0f;
+  return f32x2{u.x > 0.0f ? u.x : e.x, u.y > 0.0f ? u.y : e.y};
+}
+
+// v = hi + 2^-11 lo, both fp16 (RNE)
+__device__ __forceinline__ void split2(f32x2 v, f16x2& h, f16x2& l) {
+  h = __builtin_convertvector(v, f16x2);
+  const f32x2 hf = __builtin_convertvector(h, f32x2);
+  l = __builtin_convertvector((v - hf) * LO_SCALE, f16x2);
+}
+
+template <int CIN, int C, int WN, bool POOL>
+struct Geo {
+  static constexpr int XR = TH + 5, XC = TW + 2, XNP = XR * XC;   // input halo: rows h0-2.., cols w0-1..
+  static constexpr int TR = TH + 3;                                // t1 rows: image rows h0-1 .. h0+TH+1
+  static constexpr int LX = CIN + 8;                               // halfs per staged input pixel (+16 B)
+  static constexpr int LT = C + 8;                                 // halfs per staged t1 pixel
+  static constexpr int XHALF = XNP * LX, THALF = TR * TW * LT;
+  static constexpr int SM = XHALF > THALF ? XHALF : THALF;
+  static constexpr int WM = 4 / WN;
+  static constexpr int NTW = C / 16 / WN;           // 16-column N tiles per wave
+  static constexpr int MT1 = (TR + WM - 1) / WM;    // t1 rows per wave (GEMM 1)
+  static constexpr int MT2 = TH / WM;               // output rows per wave (GEMM 2)
+  static constexpr int KS1 = (9 * CIN + 31) / 32;   // GEMM 1 k-steps
+  static constexpr int K1PAD = KS1 * 32;
+  static constexpr int KS2 = 4 * C / 32;            // GEMM 2 k-steps
+  static constexpr int LW2 = 4 * C + 8;             // halfs per LDS row of GEMM 2's weights (+16 B)
+  static constexpr int W2 = C * LW2;
+  static constexpr int PF = 3;                      // GEMM 1 B fragments in flight (k-steps)
+  static constexpr int QPP = CIN / 4;               // float4 per halo pixel
+  static constexpr int MAXT = (XNP * QPP + NT - 1) / NT;
+  static_assert(CIN % 16 == 0 && C % 16 == 0 && (C / 16) % WN == 0, "tile shape");
+  static_assert(!POOL || MT2 % 2 == 0, "pool windows need row pairs in one wave");
+  static_assert(NT % QPP == 0, "a thread's channel quad is fixed");
+};
+
+struct TilePos {
+  int64_t clip;
+  int h0, w0;
+};
+__device__ __forceinline__ TilePos tile_pos(const ResBlkArgs& a, int id) {
+  const int tiles = a.tiles_h * a.tiles_w;
+  const int clip = id / tiles;
+  const int t = id - clip * tiles;
+  const int th_i = t / a.tiles_w;
+  return {clip, th_i * TH, (t - th_i * a.tiles_w) * TW};
+}
+
+// issue this thread's halo loads of tile p (registers; consumed by stage_halo)
+template <int CIN, int C, int WN, bool POOL>
+__device__ __forceinline__ void load_halo(const ResBlkArgs& a, TilePos p, int tid,
+                                          float4 (&pre)[Geo<CIN, C, WN, POOL>::MAXT],
+                                          uint32_t& valid) {
+  using G = Geo<CIN, C, WN, POOL>;
+  const int q = tid % G::QPP;
+  const float* xc = a.x + p.clip * a.h * a.w * CIN + 4 * q;
+  valid = 0;
+#pragma unroll
+  for (int j = 0; j < G::MAXT; ++j) {
+    const int px = (tid + j * NT) / G::QPP;
+    pre[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (px < G::XNP) {
+      const int py = px / G::XC, pxx = px - (px / G::XC) * G::XC;
+      const int ih = p.h0 - 2 + py, iw = p.w0 - 1 + pxx;
+      if (ih >= 0 && ih < a.h && iw >= 0 && iw < a.w) {
+#if RB_EXP == 1
+        pre[j] = make_float4(0.01f * ih, 0.02f * iw, 0.f, 1.f);
+#else
+        pre[j] = *reinterpret_cast<const float4*>(xc + (ih * a.w + iw) * CIN);
+#endif
+        valid |= 1u << j;
+      }
+    }
+  }
+}
+
+template <int CIN, int C, int WN, bool POOL>
+__global__ void __launch_bounds__(NT, 2) resblk_kernel(ResBlkArgs a, int total) {
+  using G = Geo<CIN, C, WN, POOL>;
+  constexpr int XC = G::XC, TR = G::TR, LX = G::LX, LT = G::LT, MT1 = G::MT1, MT2 = G::MT2;
+  constexpr int NTW = G::NTW, KS1 = G::KS1, K1PAD = G::K1PAD, KS2 = G::KS2, PF = G::PF;
+  constexpr int QPP = G::QPP, MAXT = G::MAXT;
+  // [halo | t1] hi, [halo | t1] lo, GEMM 2 weights hi, lo (resident for the whole launch)
+  __shared__ __attribute__((aligned(16))) _Float16 smem[2 * G::SM + 2 * G::W2];
+  _Float16* const s_hi = smem;
+  _Float16* const s_lo = smem + G::SM;
+  _Float16* const s_w2h = smem + 2 * G::SM;
+  _Float16* const s_w2l = s_w2h + G::W2;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // SGPR: per-wave branches are scalar
+  const int wn = wave % WN, wm = wave / WN;
+  const int col = lane & 15, grp = lane >> 4;
+
+  // per-thread constants: BN1 of this thread's channel quad, B row pointers, BN2 / biases per column
+  const int q = tid % QPP;
+  const float4 sc4 = *reinterpret_cast<const float4*>(a.s1 + 4 * q);
+  const float4 sh4 = *reinterpret_cast<const float4*>(a.t1 + 4 * q);
+  const f32x2 sc01 = {sc4.x, sc4.y}, sc23 = {sc4.z, sc4.w};
+  const f32x2 sh01 = {sh4.x, sh4.y}, sh23 = {sh4.z, sh4.w};
+  int b1o[NTW], b2o[NTW];   // this lane's B fragment offsets (GEMM 1: global, GEMM 2: LDS)
+#pragma unroll
+  for (int nt = 0; nt < NTW; ++nt) {
+    const int co = (wn * NTW + nt) * 16 + col;
+    b1o[nt] = co * K1PAD + 8 * grp;
+    b2o[nt] = co * G::LW2 + 8 * grp;
+  }
+  // GEMM 2's weights -> LDS once per workgroup (16-B pieces; rows padded to spread the banks)
+  for (int i = tid; i < C * (4 * C / 8); i += NT) {
+    const int co = i / (4 * C / 8), k8 = i - co * (4 * C / 8);
+    *reinterpret_cast<f16x8*>(s_w2h + co * G::LW2 + 8 * k8) =
+        *reinterpret_cast<const f16x8*>(a.w2h + co * 4 * C + 8 * k8);
+    *reinterpret_cast<f16x8*>(s_w2l + co * G::LW2 + 8 * k8) =
+        *reinterpret_cast<const f16x8*>(a.w2l + co * 4 * C + 8 * k8);
+  }
+
+  {
+    const int id = blockIdx.x;
+    const TilePos p = tile_pos(a, id);
+    float4 pre[MAXT];
+    uint32_t valid = 0;
+    load_halo<CIN, C, WN, POOL>(a, p, tid, pre, valid);
+
+    // ---- stage the halo: BN1 + ELU once per element, split hi/lo, zero outside the image ---------
+#pragma unroll
+    for (int j = 0; j < MAXT; ++j) {
+      const int px = (tid + j * NT) / QPP;
+      if (px >= G::XNP) continue;
+      f32x2 v01 = {pre[j].x, pre[j].y}, v23 = {pre[j].z, pre[j].w};
+      const bool ok = (valid >> j) & 1u;   // outside the image the conv input is the zero padding
+      const f32x2 u01 = elu2(v01 * sc01 + sh01), u23 = elu2(v23 * sc23 + sh23);
+      v01 = ok ? u01 : f32x2{0.f, 0.f};
+      v23 = ok ? u23 : f32x2{0.f, 0.f};
+      f16x2 h01, l01, h23, l23;
+      split2(v01, h01, l01);
+      split2(v23, h23, l23);
+      const f16x4 hv = {h01.x, h01.y, h23.x, h23.y};
+      const f16x4 lv = {l01.x, l01.y, l23.x, l23.y};
+      *reinterpret_cast<f16x4*>(s_hi + px * LX + 4 * q) = hv;
+      *reinterpret_cast<f16x4*>(s_lo + px * LX + 4 * q) = lv;
+    }
+    __syncthreads();
+
+    // ---- GEMM 1: t1 rows [wm * MT1, +MT1) x this wave's N tiles, K = (tap, ci) --------------------
+    f32x4 acc1[MT1][NTW], acc2[MT1][NTW];
+#pragma unroll
+    for (int m = 0; m < MT1; ++m)
+#pragma unroll
+      for (int nt = 0; nt < NTW; ++nt) {
+        acc1[m][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        acc2[m][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    f16x8 bh[PF][NTW], bl[PF][NTW];     // ring of B fragments, PF k-steps ahead
+#pragma unroll
+    for (int s = 0; s < PF && s < KS1; ++s)
+#pragma unroll
+      for (int nt = 0; nt < NTW; ++nt) {
+        bh[s][nt] = *reinterpret_cast<const f16x8*>(a.w1h + b1o[nt] + 32 * s);
+        bl[s][nt] = *reinterpret_cast<const f16x8*>(a.w1l + b1o[nt] + 32 * s);
+      }
+#pragma unroll
+    for (int s = 0; s < KS1; ++s) {
+      const int kk = 32 * s + 8 * grp;
+      int tap = kk / CIN;
+      const int ci = kk - tap * CIN;
+      tap = tap > 8 ? 8 : tap;               // k >= 9 * CIN: zero weights, any finite A
+      const int dy = tap / 3, dx = tap - (tap / 3) * 3;
+      const int aoff = (dy * XC + dx + col) * LX + ci;
+      f16x8 ch[NTW], cl[NTW];
+#pragma unroll
+      for (int nt = 0; nt < NTW; ++nt) {
+        ch[nt] = bh[s % PF][nt];
+        cl[nt] = bl[s % PF][nt];
+      }
+      if (s + PF < KS1) {
+#pragma unroll
+        for (int nt = 0; nt < NTW; ++nt) {
+          bh[s % PF][nt] = *reinterpret_cast<const f16x8*>(a.w1h + b1o[nt] + 32 * (s + PF));
+          bl[s % PF][nt] = *reinterpret_cast<const f16x8*>(a.w1l + b1o[nt] + 32 * (s + PF));
+        }
+      }
+#pragma unroll
+      for (int m = 0; m < MT1; ++m) {
+        const int t = wm * MT1 + m;
+        if (t >= TR) continue;
+        const int off = t * XC * LX + aoff;
+        const f16x8 ah = *reinterpret_cast<const f16x8*>(s_hi + off);
+        const f16x8 al = *reinterpret_cast<const f16x8*>(s_lo + off);
+#pragma unroll
+        for (int nt = 0; nt < NTW; ++nt) {
+#if RB_EXP == 2
+          acc1[m][nt][0] += (float)ah[0] * (float)ch[nt][0];
+          acc2[m][nt][0] += (float)al[0] * (float)cl[nt][0];
+          continue;
+#endif
+          acc1[m][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, ch[nt], acc1[m][nt], 0, 0, 0);
+          acc2[m][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, cl[nt], acc2[m][nt], 0, 0, 0);
+          acc2[m][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, ch[nt], acc2[m][nt], 0, 0, 0);
+        }
+      }
+    }
+    __syncthreads();   // every wave is done with the input halo: its LDS now takes t1
+
+    // ---- t1 -> LDS: BN2(acc + b1) + ELU, zero on rows outside the image ('same' pad of (4,1)) ----
+    // BN2(v + b1) = acc1 * s2 + acc2 * (2^-11 s2) + (b1 s2 + t2): two v_pk_fma_f32 per pixel pair
+#pragma unroll
+    for (int nt = 0; nt < NTW; ++nt) {
+      const int n = (wn * NTW + nt) * 16 + col;
+      const float s2 = a.s2[n];
+      const float c2 = fmaf(a.b1[n], s2, a.t2[n]);
+      const f32x2 s2v = {s2, s2}, s2l = {s2 * LO_INV, s2 * LO_INV}, c2v = {c2, c2};
+#pragma unroll
+      for (int m = 0; m < MT1; ++m) {
+        const int t = wm * MT1 + m;            // scalar
+        if (t >= TR) continue;
+        const int ih = p.h0 - 1 + t;
+        const bool inside = ih >= 0 && ih < a.h;
+#pragma unroll
+        for (int i = 0; i < 4; i += 2) {
+          f32x2 v = {0.f, 0.f};
+#if RB_EXP == 3
+          if (inside) v = f32x2{acc1[m][nt][i], acc2[m][nt][i + 1]};
+          s_hi[(t * TW + 4 * grp + i) * LT + n] = (_Float16)v.x;
+          s_lo[(t * TW + 4 * grp + i) * LT + n] = (_Float16)v.y;
+          continue;
+#endif
+          if (inside) {
+            const f32x2 x1 = {acc1[m][nt][i], acc1[m][nt][i + 1]};
+            const f32x2 x2 = {acc2[m][nt][i], acc2[m][nt][i + 1]};
+            v = elu2(x1 * s2v + (x2 * s2l + c2v));
+          }
+          f16x2 hv, lv;
+          split2(v, hv, lv);
+          const int o = (t * TW + 4 * grp + i) * LT + n;
+          s_hi[o] = hv.x;
+          s_lo[o] = lv.x;
+          s_hi[o + LT] = hv.y;
+          s_lo[o + LT] = lv.y;
+        }
+      }
+    }
+    __syncthreads();
+
+    // ---- GEMM 2: output rows [wm * MT2, +MT2), K = (dy, ci) over t1 rows r + dy ------------------
+    f32x4 d1[MT2][NTW], d2[MT2][NTW];
+#pragma unroll
+    for (int m = 0; m < MT2; ++m)
+#pragma unroll
+      for (int nt = 0; nt < NTW; ++nt) {
+        d1[m][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        d2[m][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+    for (int s = 0; s < KS2; ++s) {
+      const int kk = 32 * s + 8 * grp;
+      const int dy = kk / C, ci = kk - (kk / C) * C;
+      const int aoff = (dy * TW + col) * LT + ci;
+      f16x8 gh[NTW], gl[NTW];
+#pragma unroll
+      for (int nt = 0; nt < NTW; ++nt) {
+        gh[nt] = *reinterpret_cast<const f16x8*>(s_w2h + b2o[nt] + 32 * s);
+        gl[nt] = *reinterpret_cast<const f16x8*>(s_w2l + b2o[nt] + 32 * s);
+      }
+#pragma unroll
+      for (int m = 0; m < MT2; ++m) {
+        const int r = wm * MT2 + m;
+        const int off = r * TW * LT + aoff;
+        const f16x8 ah = *reinterpret_cast<const f16x8*>(s_hi + off);
+        const f16x8 al = *reinterpret_cast<const f16x8*>(s_lo + off);
+#pragma unroll
+        for (int nt = 0; nt < NTW; ++nt) {
+#if RB_EXP == 2
+          d1[m][nt][0] += (float)ah[0] * (float)gh[nt][0];
+          d2[m][nt][0] += (float)al[0] * (float)gl[nt][0];
+          continue;
+#endif
+          d1[m][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, gh[nt], d1[m][nt], 0, 0, 0);
+          d2[m][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, gl[nt], d2[m][nt], 0, 0, 0);
+          d2[m][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, gh[nt], d2[m][nt], 0, 0, 0);
+        }
+      }
+    }
+
+    // ---- epilogue: + b2, then residual add or 2x2 max pool straight from the accumulators --------
+#pragma unroll
+    for (int nt = 0; nt < NTW; ++nt) {
+      const int n = (wn * NTW + nt) * 16 + col;
+      const float b = a.b2[n];
+      if constexpr (POOL) {
+        const int hp = (a.h + 1) >> 1, wp = (a.w + 1) >> 1;
+#pragma unroll
+        for (int m = 0; m < MT2; m += 2) {
+          const int oh = p.h0 + wm * MT2 + m;     // even
+          if (oh >= a.h) continue;
+          const bool row2 = oh + 1 < a.h;
+#pragma unroll
+          for (int e = 0; e < 4; e += 2) {
+            const int ow = p.w0 + 4 * grp + e;    // even
+            if (ow >= a.w) continue;
+            const bool col2 = ow + 1 < a.w;
+            float mx = d1[m][nt][e] + d2[m][nt][e] * LO_INV;
+            if (col2) mx = fmaxf(mx, d1[m][nt][e + 1] + d2[m][nt][e + 1] * LO_INV);
+            if (row2) {
+              mx = fmaxf(mx, d1[m + 1][nt][e] + d2[m + 1][nt][e] * LO_INV);
+              if (col2) mx = fmaxf(mx, d1[m + 1][nt][e + 1] + d2[m + 1][nt][e + 1] * LO_INV);
+            }
+            a.y[((p.clip * hp + (oh >> 1)) * wp + (ow >> 1)) * C + n] = mx + b;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int m = 0; m < MT2; ++m) {
+          const int oh = p.h0 + wm * MT2 + m;
+          if (oh >= a.h) continue;
+          const int64_t rowbase = (p.clip * a.h + oh) * a.w;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int ow = p.w0 + 4 * grp + i;
+            if (ow >= a.w) continue;
+            const int64_t o = (rowbase + ow) * C + n;
+            a.y[o] = d1[m][nt][i] + d2[m][nt][i] * LO_INV + b + a.x[o];
+          }
+        }
+      }
+    }
+  }
+}
+
+template <int CIN, int C, int WN, bool POOL>
+hipError_t launch(const ResBlkArgs& a, hipStream_t s) {
+  const int total = a.n * a.tiles_h * a.tiles_w;
+  hipLaunchKernelGGL((resblk_kernel<CIN, C, WN, POOL>), dim3(total), dim3(NT), 0, s, a, total);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+int resblk_k1pad(int cin) { return (9 * cin + 31) / 32 * 32; }
+
+bool resblk_supported(int cin, int c, bool pool) {
+  return c == 32 && ((cin == 16 && pool) || (cin == 32 && !pool));
+}
+
+hipError_t resblk_launch(ResBlkArgs a, int cin, int c, bool pool, hipStream_t s) {
+  if ((int64_t)a.n * a.h * a.w == 0) return hipSuccess;
+  if (!resblk_supported(cin, c, pool)) return hipErrorInvalidValue;
+  a.tiles_h = (a.h + TH - 1) / TH;
+  a.tiles_w = (a.w + TW - 1) / TW;
+  if ((int64_t)a.n * a.tiles_h * a.tiles_w > 0x7fffffffLL) return hipErrorInvalidValue;
+  if (cin == 16) return launch<16, 32, 2, true>(a, s);
+  return launch<32, 32, 2, false>(a, s);
+}
+
+static uint16_t f16_bits(float f) {
+  _Float16 h = (_Float16)f;
+  uint16_t b;
+  memcpy(&b, &h, 2);
+  return b;
+}
+
+void resblk_split_weights(const float* w, int taps, int cin, int cout, int kpad, uint16_t* hi,
+                          uint16_t* lo) {
+  for (size_t i = 0; i < (size_t)cout * kpad; ++i) hi[i] = lo[i] = 0;
+  for (int t = 0; t < taps; ++t)
+    for (int ci = 0; ci < cin; ++ci)
+      for (int co = 0; co < cout; ++co) {
+        const float v = w[((size_t)t * cin + ci) * cout + co];
+        const _Float16 h = (_Float16)v;
+        const size_t o = (size_t)co * kpad + (size_t)t * cin + ci;
+        hi[o] = f16_bits(v);
+        lo[o] = f16_bits((v - (float)h) * LO_SCALE);
+      }
+}
