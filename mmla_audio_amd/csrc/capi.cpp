@@ -258,7 +258,7 @@ int take_conv(mmla_ctx* c, Cursor& cur, std::vector<void*>& al, int kh, int kw, 
     CHK(upload(c, al, lo.data(), n * sizeof(uint16_t), &p));
     w->wl = reinterpret_cast<uint16_t*>(p);
   }
-  if (kh * kw > 1 && cin % 16 == 0 && cout % 16 == 0) {
+  if (cin % 16 == 0 && cout % 16 == 0) {   // fused res_block layout (resblk.hip)
     w->kpad = (kh * kw * cin + 31) / 32 * 32;
     const size_t n = (size_t)cout * w->kpad;
     std::vector<uint16_t> hi(n), lo(n);
@@ -484,6 +484,7 @@ int run_od_net(mmla_ctx* c, const uint8_t* img_u8, const float* img_f32, int64_t
   for (int b = 0; b < 9; ++b) {   // res_block, overlap_detector_temp.py:253-277
     const OdBlock& B = W.blk[b];
     if (c->precision == MMLA_PREC_F16X3 && B.c3.fh && B.c4.fh && B.c4.kpad == 4 * B.c4.cin &&
+        (!POOL[b] || B.sc.fh) &&
         resblk_supported(B.c3.cin, B.c3.cout, POOL[b])) {
       // whole block in one launch: t1 stays in LDS (resblk.hip)
       ResBlkArgs r{};
@@ -498,15 +499,20 @@ int run_od_net(mmla_ctx* c, const uint8_t* img_u8, const float* img_f32, int64_t
       r.b2 = B.c4.bias;
       r.s2 = B.bn_mid.scale;
       r.t2 = B.bn_mid.shift;
-      r.y = POOL[b] ? T2 : T1;
+      if (POOL[b]) {
+        r.wsh = B.sc.fh;
+        r.wsl = B.sc.fl;
+        r.bs = B.sc.bias;
+      }
+      r.y = T1;
       r.n = (int)n;
       r.h = h;
       r.w = w;
       LAUNCH(c, MMLA_STAGE_CONV,
-             2.0 * n * h * w * (9.0 * B.c3.cin * B.c3.cout + 4.0 * B.c4.cin * B.c4.cout),
+             2.0 * n * h * w * (9.0 * B.c3.cin * B.c3.cout + 4.0 * B.c4.cin * B.c4.cout) +
+                 (POOL[b] ? 2.0 * n * ((h + 1) / 2) * ((w + 1) / 2) * B.sc.cin * B.sc.cout : 0.0),
              resblk_launch(r, B.c3.cin, B.c3.cout, POOL[b], c->stream));
-      if (POOL[b]) {   // + Conv2D(1x1, stride 2)(x)
-        CHK(conv_run(c, conv_args(B.sc, X, T1, (int)n, h, w, 2, nullptr, PRO_NONE, EPI_ADD, T2)));
+      if (POOL[b]) {
         h = (h + 1) / 2;
         w = (w + 1) / 2;
       }

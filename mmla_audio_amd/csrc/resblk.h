@@ -15,8 +15,11 @@ struct ResBlkArgs {
   const float* b2;         // [C]
   const float* s2;         // BatchNorm before the (4,1) conv, folded [C]
   const float* t2;
+  const uint16_t* wsh;     // pool blocks: Conv2D(1x1, stride 2) shortcut, fp16 hi [C][KSC], k = ci
+  const uint16_t* wsl;     //   (KSC = CIN rounded up to 32)
+  const float* bs;         //   shortcut bias [C]
   float* y;                // non-pool: [N, H, W, C] = x + conv;  pool: [N, ceil(H/2), ceil(W/2), C]
-  int n, h, w;             // = MaxPool2D(2, 'same')(conv)   (the 1x1/2 shortcut is added after)
+  int n, h, w;             //   = MaxPool2D(2, 'same')(conv) + Conv2D(1x1, stride 2)(x)
   int tiles_h, tiles_w;    // set by resblk_launch
 };
 

@@ -60,78 +60,41 @@ __device__ __forceinline__ void split2(f32x2 v, f16x2& h, f16x2& l) {
   l = __builtin_convertvector((v - hf) * LO_SCALE, f16x2);
 }
 
-template <int CIN, int C, int WN, bool POOL>
+template <int CIN, int C, bool POOL>
 struct Geo {
-  static constexpr int XR = TH + 5, XC = TW + 2, XNP = XR * XC;   // input halo: rows h0-2.., cols w0-1..
-  static constexpr int TR = TH + 3;                                // t1 rows: image rows h0-1 .. h0+TH+1
-  static constexpr int LX = CIN + 8;                               // halfs per staged input pixel (+16 B)
-  static constexpr int LT = C + 8;                                 // halfs per staged t1 pixel
-  static constexpr int XHALF = XNP * LX, THALF = TR * TW * LT;
+  static constexpr int WN = C / 16 >= 2 ? 2 : 1;   // waves along N (16-column tiles)
+  static constexpr int WM = 4 / WN;                // waves along M (tile rows)
+  static constexpr int NTW = C / 16 / WN;          // N tiles per wave
+  static constexpr int TR = TH + 3;                // t1 rows needed: image rows h0-1 .. h0+TH+1
+  static constexpr int TRP = (TR + WM - 1) / WM * WM;   // computed (padded: no per-row branches)
+  static constexpr int XR = TRP + 2, XC = TW + 2, XNP = XR * XC;   // input halo rows h0-2.., cols w0-1..
+  static constexpr int LX = CIN + 8;               // halfs per staged input pixel (+16 B: banks)
+  static constexpr int LT = C + 8;                 // halfs per staged t1 pixel
+  static constexpr int XHALF = XNP * LX, THALF = TRP * TW * LT;
   static constexpr int SM = XHALF > THALF ? XHALF : THALF;
-  static constexpr int WM = 4 / WN;
-  static constexpr int NTW = C / 16 / WN;           // 16-column N tiles per wave
-  static constexpr int MT1 = (TR + WM - 1) / WM;    // t1 rows per wave (GEMM 1)
-  static constexpr int MT2 = TH / WM;               // output rows per wave (GEMM 2)
-  static constexpr int KS1 = (9 * CIN + 31) / 32;   // GEMM 1 k-steps
+  static constexpr int MT1 = TRP / WM;             // t1 rows per wave (GEMM 1)
+  static constexpr int MT2 = TH / WM;              // output rows per wave (GEMM 2)
+  static constexpr int KS1 = (9 * CIN + 31) / 32;  // GEMM 1 k-steps
   static constexpr int K1PAD = KS1 * 32;
-  static constexpr int KS2 = 4 * C / 32;            // GEMM 2 k-steps
-  static constexpr int LW2 = 4 * C + 8;             // halfs per LDS row of GEMM 2's weights (+16 B)
+  static constexpr int KS2 = 4 * C / 32;           // GEMM 2 k-steps
+  static constexpr int KSC = (CIN + 31) / 32;      // shortcut (1x1) k-steps
+  static constexpr int LW2 = 4 * C + 8;            // halfs per LDS row of GEMM 2's weights
   static constexpr int W2 = C * LW2;
-  static constexpr int PF = 3;                      // GEMM 1 B fragments in flight (k-steps)
-  static constexpr int QPP = CIN / 4;               // float4 per halo pixel
+  static constexpr int PF = 3;                     // GEMM 1 B fragments in flight (k-steps)
+  static constexpr int QPP = CIN / 4;              // float4 per halo pixel
   static constexpr int MAXT = (XNP * QPP + NT - 1) / NT;
-  static_assert(CIN % 16 == 0 && C % 16 == 0 && (C / 16) % WN == 0, "tile shape");
-  static_assert(!POOL || MT2 % 2 == 0, "pool windows need row pairs in one wave");
+  static_assert(CIN % 16 == 0 && C % 16 == 0, "channel tiles");
+  static_assert(!POOL || MT2 % 4 == 0, "pooled shortcut tiles need 4 output rows per wave");
   static_assert(NT % QPP == 0, "a thread's channel quad is fixed");
 };
 
-struct TilePos {
-  int64_t clip;
-  int h0, w0;
-};
-__device__ __forceinline__ TilePos tile_pos(const ResBlkArgs& a, int id) {
-  const int tiles = a.tiles_h * a.tiles_w;
-  const int clip = id / tiles;
-  const int t = id - clip * tiles;
-  const int th_i = t / a.tiles_w;
-  return {clip, th_i * TH, (t - th_i * a.tiles_w) * TW};
-}
-
-// issue this thread's halo loads of tile p (registers; consumed by stage_halo)
-template <int CIN, int C, int WN, bool POOL>
-__device__ __forceinline__ void load_halo(const ResBlkArgs& a, TilePos p, int tid,
-                                          float4 (&pre)[Geo<CIN, C, WN, POOL>::MAXT],
-                                          uint32_t& valid) {
-  using G = Geo<CIN, C, WN, POOL>;
-  const int q = tid % G::QPP;
-  const float* xc = a.x + p.clip * a.h * a.w * CIN + 4 * q;
-  valid = 0;
-#pragma unroll
-  for (int j = 0; j < G::MAXT; ++j) {
-    const int px = (tid + j * NT) / G::QPP;
-    pre[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (px < G::XNP) {
-      const int py = px / G::XC, pxx = px - (px / G::XC) * G::XC;
-      const int ih = p.h0 - 2 + py, iw = p.w0 - 1 + pxx;
-      if (ih >= 0 && ih < a.h && iw >= 0 && iw < a.w) {
-#if RB_EXP == 1
-        pre[j] = make_float4(0.01f * ih, 0.02f * iw, 0.f, 1.f);
-#else
-        pre[j] = *reinterpret_cast<const float4*>(xc + (ih * a.w + iw) * CIN);
-#endif
-        valid |= 1u << j;
-      }
-    }
-  }
-}
-
-template <int CIN, int C, int WN, bool POOL>
-__global__ void __launch_bounds__(NT, 2) resblk_kernel(ResBlkArgs a, int total) {
-  using G = Geo<CIN, C, WN, POOL>;
-  constexpr int XC = G::XC, TR = G::TR, LX = G::LX, LT = G::LT, MT1 = G::MT1, MT2 = G::MT2;
-  constexpr int NTW = G::NTW, KS1 = G::KS1, K1PAD = G::K1PAD, KS2 = G::KS2, PF = G::PF;
-  constexpr int QPP = G::QPP, MAXT = G::MAXT;
-  // [halo | t1] hi, [halo | t1] lo, GEMM 2 weights hi, lo (resident for the whole launch)
+template <int CIN, int C, bool POOL>
+__global__ void __launch_bounds__(NT, 2) resblk_kernel(ResBlkArgs a) {
+  using G = Geo<CIN, C, POOL>;
+  constexpr int XC = G::XC, LX = G::LX, LT = G::LT, MT1 = G::MT1, MT2 = G::MT2, NTW = G::NTW;
+  constexpr int KS1 = G::KS1, K1PAD = G::K1PAD, KS2 = G::KS2, PF = G::PF, QPP = G::QPP;
+  constexpr int MAXT = G::MAXT, WN = G::WN;
+  // [halo | t1] hi, [halo | t1] lo, GEMM 2 weights hi, lo
   __shared__ __attribute__((aligned(16))) _Float16 smem[2 * G::SM + 2 * G::W2];
   _Float16* const s_hi = smem;
   _Float16* const s_lo = smem + G::SM;
@@ -139,24 +102,40 @@ __global__ void __launch_bounds__(NT, 2) resblk_kernel(ResBlkArgs a, int total) 
   _Float16* const s_w2l = s_w2h + G::W2;
 
   const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // SGPR: per-wave branches are scalar
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // SGPR: per-wave values are scalar
   const int wn = wave % WN, wm = wave / WN;
   const int col = lane & 15, grp = lane >> 4;
+  const int tiles = a.tiles_h * a.tiles_w;
+  const int clip = blockIdx.x / tiles;
+  const int tile = blockIdx.x - clip * tiles;
+  const int th_i = tile / a.tiles_w;
+  const int h0 = th_i * TH, w0 = (tile - th_i * a.tiles_w) * TW;
 
-  // per-thread constants: BN1 of this thread's channel quad, B row pointers, BN2 / biases per column
+  // ---- issue the halo loads (all in flight at once) ----------------------------------------------
   const int q = tid % QPP;
-  const float4 sc4 = *reinterpret_cast<const float4*>(a.s1 + 4 * q);
-  const float4 sh4 = *reinterpret_cast<const float4*>(a.t1 + 4 * q);
-  const f32x2 sc01 = {sc4.x, sc4.y}, sc23 = {sc4.z, sc4.w};
-  const f32x2 sh01 = {sh4.x, sh4.y}, sh23 = {sh4.z, sh4.w};
-  int b1o[NTW], b2o[NTW];   // this lane's B fragment offsets (GEMM 1: global, GEMM 2: LDS)
+  float4 pre[MAXT];
+  uint32_t valid = 0;
+  {
+    const float* xc = a.x + (int64_t)clip * a.h * a.w * CIN + 4 * q;
 #pragma unroll
-  for (int nt = 0; nt < NTW; ++nt) {
-    const int co = (wn * NTW + nt) * 16 + col;
-    b1o[nt] = co * K1PAD + 8 * grp;
-    b2o[nt] = co * G::LW2 + 8 * grp;
+    for (int j = 0; j < MAXT; ++j) {
+      const int px = (tid + j * NT) / QPP;
+      pre[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (px < G::XNP) {
+        const int py = px / XC, pxx = px - (px / XC) * XC;
+        const int ih = h0 - 2 + py, iw = w0 - 1 + pxx;
+        if (ih >= 0 && ih < a.h && iw >= 0 && iw < a.w) {
+#if RB_EXP == 1
+          pre[j] = make_float4(0.01f * ih, 0.02f * iw, 0.f, 1.f);
+#else
+          pre[j] = *reinterpret_cast<const float4*>(xc + (ih * a.w + iw) * CIN);
+#endif
+          valid |= 1u << j;
+        }
+      }
+    }
   }
-  // GEMM 2's weights -> LDS once per workgroup (16-B pieces; rows padded to spread the banks)
+  // GEMM 2's weights -> LDS (16-B pieces; rows padded to spread the banks)
   for (int i = tid; i < C * (4 * C / 8); i += NT) {
     const int co = i / (4 * C / 8), k8 = i - co * (4 * C / 8);
     *reinterpret_cast<f16x8*>(s_w2h + co * G::LW2 + 8 * k8) =
@@ -165,20 +144,18 @@ __global__ void __launch_bounds__(NT, 2) resblk_kernel(ResBlkArgs a, int total) 
         *reinterpret_cast<const f16x8*>(a.w2l + co * 4 * C + 8 * k8);
   }
 
+  // ---- stage: BN1 + ELU once per element, split hi/lo; zero outside the image (conv padding) ----
   {
-    const int id = blockIdx.x;
-    const TilePos p = tile_pos(a, id);
-    float4 pre[MAXT];
-    uint32_t valid = 0;
-    load_halo<CIN, C, WN, POOL>(a, p, tid, pre, valid);
-
-    // ---- stage the halo: BN1 + ELU once per element, split hi/lo, zero outside the image ---------
+    const float4 sc4 = *reinterpret_cast<const float4*>(a.s1 + 4 * q);
+    const float4 sh4 = *reinterpret_cast<const float4*>(a.t1 + 4 * q);
+    const f32x2 sc01 = {sc4.x, sc4.y}, sc23 = {sc4.z, sc4.w};
+    const f32x2 sh01 = {sh4.x, sh4.y}, sh23 = {sh4.z, sh4.w};
 #pragma unroll
     for (int j = 0; j < MAXT; ++j) {
       const int px = (tid + j * NT) / QPP;
       if (px >= G::XNP) continue;
       f32x2 v01 = {pre[j].x, pre[j].y}, v23 = {pre[j].z, pre[j].w};
-      const bool ok = (valid >> j) & 1u;   // outside the image the conv input is the zero padding
+      const bool ok = (valid >> j) & 1u;
       const f32x2 u01 = elu2(v01 * sc01 + sh01), u23 = elu2(v23 * sc23 + sh23);
       v01 = ok ? u01 : f32x2{0.f, 0.f};
       v23 = ok ? u23 : f32x2{0.f, 0.f};
@@ -190,33 +167,38 @@ __global__ void __launch_bounds__(NT, 2) resblk_kernel(ResBlkArgs a, int total) 
       *reinterpret_cast<f16x4*>(s_hi + px * LX + 4 * q) = hv;
       *reinterpret_cast<f16x4*>(s_lo + px * LX + 4 * q) = lv;
     }
-    __syncthreads();
+  }
+  __syncthreads();
 
-    // ---- GEMM 1: t1 rows [wm * MT1, +MT1) x this wave's N tiles, K = (tap, ci) --------------------
-    f32x4 acc1[MT1][NTW], acc2[MT1][NTW];
+  // ---- GEMM 1: t1 rows [wm * MT1, +MT1) x this wave's N tiles, K = (tap, ci) ----------------------
+  f32x4 acc1[MT1][NTW], acc2[MT1][NTW];
 #pragma unroll
-    for (int m = 0; m < MT1; ++m)
+  for (int m = 0; m < MT1; ++m)
 #pragma unroll
-      for (int nt = 0; nt < NTW; ++nt) {
-        acc1[m][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-        acc2[m][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-      }
-    f16x8 bh[PF][NTW], bl[PF][NTW];     // ring of B fragments, PF k-steps ahead
+    for (int nt = 0; nt < NTW; ++nt) {
+      acc1[m][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      acc2[m][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  {
+    const int b1o = ((wn * NTW) * 16 + col) * K1PAD + 8 * grp;   // + nt * 16 * K1PAD
+    f16x8 bh[PF][NTW], bl[PF][NTW];   // ring of B fragments, PF k-steps ahead
 #pragma unroll
     for (int s = 0; s < PF && s < KS1; ++s)
 #pragma unroll
       for (int nt = 0; nt < NTW; ++nt) {
-        bh[s][nt] = *reinterpret_cast<const f16x8*>(a.w1h + b1o[nt] + 32 * s);
-        bl[s][nt] = *reinterpret_cast<const f16x8*>(a.w1l + b1o[nt] + 32 * s);
+        bh[s][nt] = *reinterpret_cast<const f16x8*>(a.w1h + b1o + nt * 16 * K1PAD + 32 * s);
+        bl[s][nt] = *reinterpret_cast<const f16x8*>(a.w1l + b1o + nt * 16 * K1PAD + 32 * s);
       }
+    const _Float16* ahb = s_hi + (wm * MT1 * XC + col) * LX;   // + m * XC * LX (immediate)
+    const _Float16* alb = s_lo + (wm * MT1 * XC + col) * LX;
 #pragma unroll
     for (int s = 0; s < KS1; ++s) {
       const int kk = 32 * s + 8 * grp;
       int tap = kk / CIN;
       const int ci = kk - tap * CIN;
-      tap = tap > 8 ? 8 : tap;               // k >= 9 * CIN: zero weights, any finite A
+      tap = tap > 8 ? 8 : tap;                 // k >= 9 * CIN: zero weights, any finite A
       const int dy = tap / 3, dx = tap - (tap / 3) * 3;
-      const int aoff = (dy * XC + dx + col) * LX + ci;
+      const int koff = (dy * XC + dx) * LX + ci;
       f16x8 ch[NTW], cl[NTW];
 #pragma unroll
       for (int nt = 0; nt < NTW; ++nt) {
@@ -226,17 +208,14 @@ __global__ void __launch_bounds__(NT, 2) resblk_kernel(ResBlkArgs a, int total) 
       if (s + PF < KS1) {
 #pragma unroll
         for (int nt = 0; nt < NTW; ++nt) {
-          bh[s % PF][nt] = *reinterpret_cast<const f16x8*>(a.w1h + b1o[nt] + 32 * (s + PF));
-          bl[s % PF][nt] = *reinterpret_cast<const f16x8*>(a.w1l + b1o[nt] + 32 * (s + PF));
+          bh[s % PF][nt] = *reinterpret_cast<const f16x8*>(a.w1h + b1o + nt * 16 * K1PAD + 32 * (s + PF));
+          bl[s % PF][nt] = *reinterpret_cast<const f16x8*>(a.w1l + b1o + nt * 16 * K1PAD + 32 * (s + PF));
         }
       }
 #pragma unroll
       for (int m = 0; m < MT1; ++m) {
-        const int t = wm * MT1 + m;
-        if (t >= TR) continue;
-        const int off = t * XC * LX + aoff;
-        const f16x8 ah = *reinterpret_cast<const f16x8*>(s_hi + off);
-        const f16x8 al = *reinterpret_cast<const f16x8*>(s_lo + off);
+        const f16x8 ah = *reinterpret_cast<const f16x8*>(ahb + koff + m * XC * LX);
+        const f16x8 al = *reinterpret_cast<const f16x8*>(alb + koff + m * XC * LX);
 #pragma unroll
         for (int nt = 0; nt < NTW; ++nt) {
 #if RB_EXP == 2
@@ -249,11 +228,16 @@ __global__ void __launch_bounds__(NT, 2) resblk_kernel(ResBlkArgs a, int total) 
           acc2[m][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, ch[nt], acc2[m][nt], 0, 0, 0);
         }
       }
+      __builtin_amdgcn_sched_barrier(0);   // keep the scheduler's LDS-read hoisting within a k-step
     }
-    __syncthreads();   // every wave is done with the input halo: its LDS now takes t1
+  }
+  __syncthreads();   // every wave is done with the input halo: its LDS now takes t1
 
-    // ---- t1 -> LDS: BN2(acc + b1) + ELU, zero on rows outside the image ('same' pad of (4,1)) ----
-    // BN2(v + b1) = acc1 * s2 + acc2 * (2^-11 s2) + (b1 s2 + t2): two v_pk_fma_f32 per pixel pair
+  // ---- t1 -> LDS: BN2(acc + b1) + ELU; rows outside the image are the (4,1) conv's zero padding ----
+  // BN2(v + b1) = acc1 * s2 + acc2 * (2^-11 s2) + (b1 s2 + t2): two v_pk_fma_f32 per pixel pair
+  {
+    _Float16* const thb = s_hi + wm * MT1 * TW * LT + 4 * grp * LT;   // + (m * TW + i) * LT + n
+    _Float16* const tlb = s_lo + wm * MT1 * TW * LT + 4 * grp * LT;
 #pragma unroll
     for (int nt = 0; nt < NTW; ++nt) {
       const int n = (wn * NTW + nt) * 16 + col;
@@ -262,17 +246,15 @@ __global__ void __launch_bounds__(NT, 2) resblk_kernel(ResBlkArgs a, int total) 
       const f32x2 s2v = {s2, s2}, s2l = {s2 * LO_INV, s2 * LO_INV}, c2v = {c2, c2};
 #pragma unroll
       for (int m = 0; m < MT1; ++m) {
-        const int t = wm * MT1 + m;            // scalar
-        if (t >= TR) continue;
-        const int ih = p.h0 - 1 + t;
+        const int ih = h0 - 1 + wm * MT1 + m;   // scalar
         const bool inside = ih >= 0 && ih < a.h;
 #pragma unroll
         for (int i = 0; i < 4; i += 2) {
           f32x2 v = {0.f, 0.f};
 #if RB_EXP == 3
           if (inside) v = f32x2{acc1[m][nt][i], acc2[m][nt][i + 1]};
-          s_hi[(t * TW + 4 * grp + i) * LT + n] = (_Float16)v.x;
-          s_lo[(t * TW + 4 * grp + i) * LT + n] = (_Float16)v.y;
+          thb[(m * TW + i) * LT + n] = (_Float16)v.x;
+          tlb[(m * TW + i) * LT + n] = (_Float16)v.y;
           continue;
 #endif
           if (inside) {
@@ -282,42 +264,44 @@ __global__ void __launch_bounds__(NT, 2) resblk_kernel(ResBlkArgs a, int total) 
           }
           f16x2 hv, lv;
           split2(v, hv, lv);
-          const int o = (t * TW + 4 * grp + i) * LT + n;
-          s_hi[o] = hv.x;
-          s_lo[o] = lv.x;
-          s_hi[o + LT] = hv.y;
-          s_lo[o + LT] = lv.y;
+          thb[(m * TW + i) * LT + n] = hv.x;
+          tlb[(m * TW + i) * LT + n] = lv.x;
+          thb[(m * TW + i + 1) * LT + n] = hv.y;
+          tlb[(m * TW + i + 1) * LT + n] = lv.y;
         }
       }
     }
-    __syncthreads();
+  }
+  __syncthreads();
 
-    // ---- GEMM 2: output rows [wm * MT2, +MT2), K = (dy, ci) over t1 rows r + dy ------------------
-    f32x4 d1[MT2][NTW], d2[MT2][NTW];
+  // ---- GEMM 2: output rows [wm * MT2, +MT2), K = (dy, ci) over t1 rows r + dy --------------------
+  f32x4 d1[MT2][NTW], d2[MT2][NTW];
 #pragma unroll
-    for (int m = 0; m < MT2; ++m)
+  for (int m = 0; m < MT2; ++m)
 #pragma unroll
-      for (int nt = 0; nt < NTW; ++nt) {
-        d1[m][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-        d2[m][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-      }
+    for (int nt = 0; nt < NTW; ++nt) {
+      d1[m][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      d2[m][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  {
+    const _Float16* ahb = s_hi + (wm * MT2 * TW + col) * LT;
+    const _Float16* alb = s_lo + (wm * MT2 * TW + col) * LT;
+    const int b2o = ((wn * NTW) * 16 + col) * G::LW2 + 8 * grp;
 #pragma unroll
     for (int s = 0; s < KS2; ++s) {
       const int kk = 32 * s + 8 * grp;
       const int dy = kk / C, ci = kk - (kk / C) * C;
-      const int aoff = (dy * TW + col) * LT + ci;
+      const int koff = dy * TW * LT + ci;
       f16x8 gh[NTW], gl[NTW];
 #pragma unroll
       for (int nt = 0; nt < NTW; ++nt) {
-        gh[nt] = *reinterpret_cast<const f16x8*>(s_w2h + b2o[nt] + 32 * s);
-        gl[nt] = *reinterpret_cast<const f16x8*>(s_w2l + b2o[nt] + 32 * s);
+        gh[nt] = *reinterpret_cast<const f16x8*>(s_w2h + b2o + nt * 16 * G::LW2 + 32 * s);
+        gl[nt] = *reinterpret_cast<const f16x8*>(s_w2l + b2o + nt * 16 * G::LW2 + 32 * s);
       }
 #pragma unroll
       for (int m = 0; m < MT2; ++m) {
-        const int r = wm * MT2 + m;
-        const int off = r * TW * LT + aoff;
-        const f16x8 ah = *reinterpret_cast<const f16x8*>(s_hi + off);
-        const f16x8 al = *reinterpret_cast<const f16x8*>(s_lo + off);
+        const f16x8 ah = *reinterpret_cast<const f16x8*>(ahb + koff + m * TW * LT);
+        const f16x8 al = *reinterpret_cast<const f16x8*>(alb + koff + m * TW * LT);
 #pragma unroll
         for (int nt = 0; nt < NTW; ++nt) {
 #if RB_EXP == 2
@@ -330,57 +314,116 @@ __global__ void __launch_bounds__(NT, 2) resblk_kernel(ResBlkArgs a, int total) 
           d2[m][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, gh[nt], d2[m][nt], 0, 0, 0);
         }
       }
+      __builtin_amdgcn_sched_barrier(0);
     }
+  }
 
-    // ---- epilogue: + b2, then residual add or 2x2 max pool straight from the accumulators --------
+  // ---- epilogue ------------------------------------------------------------------------------------
+  const bool interior = h0 + TH <= a.h && w0 + TW <= a.w;   // scalar: no per-element bounds checks
+  if constexpr (POOL) {
+    // Conv2D(1x1, stride 2) shortcut on the raw input as a small 3xFP16 GEMM whose M rows are
+    // ordered so that its accumulator layout equals the pooled layout below: shortcut tile j of
+    // this wave, element i of lane (grp, col) = pooled row wm*MT2/2 + 2j + (i >> 1), pooled column
+    // 2 grp + (i & 1), channel col.
+    constexpr int MSC = MT2 / 4;
+    f32x4 e1[MSC][NTW], e2[MSC][NTW];
+#pragma unroll
+    for (int j = 0; j < MSC; ++j)
+#pragma unroll
+      for (int nt = 0; nt < NTW; ++nt) {
+        e1[j][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        e2[j][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    {
+      const int p = col;                          // this lane's A row (pooled pixel of the tile)
+      const int pr = (p & 3) >> 1, pc = 2 * (p >> 2) + (p & 1);
+      const float* xc = a.x + (int64_t)clip * a.h * a.w * CIN;
+#pragma unroll
+      for (int s = 0; s < G::KSC; ++s) {
+        const int ci = 32 * s + 8 * grp;
+        f16x8 bh[NTW], bl[NTW];
+#pragma unroll
+        for (int nt = 0; nt < NTW; ++nt) {
+          const int co = (wn * NTW + nt) * 16 + col;
+          bh[nt] = *reinterpret_cast<const f16x8*>(a.wsh + co * (G::KSC * 32) + ci);
+          bl[nt] = *reinterpret_cast<const f16x8*>(a.wsl + co * (G::KSC * 32) + ci);
+        }
+#pragma unroll
+        for (int j = 0; j < MSC; ++j) {
+          const int ih = h0 + 2 * (wm * (MT2 / 2) + 2 * j + pr), iw = w0 + 2 * pc;
+          float4 u0 = make_float4(0.f, 0.f, 0.f, 0.f), u1 = u0;
+          if (ci < CIN && ih < a.h && iw < a.w) {
+            const float* src = xc + (ih * a.w + iw) * CIN + ci;
+            u0 = *reinterpret_cast<const float4*>(src);
+            u1 = *reinterpret_cast<const float4*>(src + 4);
+          }
+          f16x2 h0_, l0_, h1_, l1_, h2_, l2_, h3_, l3_;
+          split2(f32x2{u0.x, u0.y}, h0_, l0_);
+          split2(f32x2{u0.z, u0.w}, h1_, l1_);
+          split2(f32x2{u1.x, u1.y}, h2_, l2_);
+          split2(f32x2{u1.z, u1.w}, h3_, l3_);
+          const f16x8 ah = {h0_.x, h0_.y, h1_.x, h1_.y, h2_.x, h2_.y, h3_.x, h3_.y};
+          const f16x8 al = {l0_.x, l0_.y, l1_.x, l1_.y, l2_.x, l2_.y, l3_.x, l3_.y};
+#pragma unroll
+          for (int nt = 0; nt < NTW; ++nt) {
+            e1[j][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh[nt], e1[j][nt], 0, 0, 0);
+            e2[j][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl[nt], e2[j][nt], 0, 0, 0);
+            e2[j][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh[nt], e2[j][nt], 0, 0, 0);
+          }
+        }
+      }
+    }
+    const int hp = (a.h + 1) >> 1, wp = (a.w + 1) >> 1;
+#pragma unroll
+    for (int nt = 0; nt < NTW; ++nt) {
+      const int n = (wn * NTW + nt) * 16 + col;
+      const float b = a.b2[n] + a.bs[n];
+#pragma unroll
+      for (int j = 0; j < MSC; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int m = 4 * j + 2 * (i >> 1);        // t2 row pair (m, m + 1) of this wave
+          const int e = 2 * (i & 1);                  // column pair (e, e + 1) of the lane's 4
+          const int oh = h0 + wm * MT2 + m, ow = w0 + 4 * grp + e;   // even
+          float mx = d1[m][nt][e] + d2[m][nt][e] * LO_INV;
+          float v01 = d1[m][nt][e + 1] + d2[m][nt][e + 1] * LO_INV;
+          float v10 = d1[m + 1][nt][e] + d2[m + 1][nt][e] * LO_INV;
+          float v11 = d1[m + 1][nt][e + 1] + d2[m + 1][nt][e + 1] * LO_INV;
+          if (!interior) {   // MaxPool2D 'same' on odd sizes: the window is cut at the edge
+            if (oh >= a.h || ow >= a.w) continue;
+            if (ow + 1 >= a.w) { v01 = mx; v11 = v10; }
+            if (oh + 1 >= a.h) { v10 = mx; v11 = v01; }
+          }
+          mx = fmaxf(fmaxf(mx, v01), fmaxf(v10, v11));
+          const float sc = e1[j][nt][i] + e2[j][nt][i] * LO_INV;
+          a.y[(((int64_t)clip * hp + (oh >> 1)) * wp + (ow >> 1)) * C + n] = mx + sc + b;
+        }
+    }
+  } else {
 #pragma unroll
     for (int nt = 0; nt < NTW; ++nt) {
       const int n = (wn * NTW + nt) * 16 + col;
       const float b = a.b2[n];
-      if constexpr (POOL) {
-        const int hp = (a.h + 1) >> 1, wp = (a.w + 1) >> 1;
 #pragma unroll
-        for (int m = 0; m < MT2; m += 2) {
-          const int oh = p.h0 + wm * MT2 + m;     // even
-          if (oh >= a.h) continue;
-          const bool row2 = oh + 1 < a.h;
+      for (int m = 0; m < MT2; ++m) {
+        const int oh = h0 + wm * MT2 + m;
+        if (!interior && oh >= a.h) continue;
+        const int64_t rowbase = ((int64_t)clip * a.h + oh) * a.w + w0 + 4 * grp;
 #pragma unroll
-          for (int e = 0; e < 4; e += 2) {
-            const int ow = p.w0 + 4 * grp + e;    // even
-            if (ow >= a.w) continue;
-            const bool col2 = ow + 1 < a.w;
-            float mx = d1[m][nt][e] + d2[m][nt][e] * LO_INV;
-            if (col2) mx = fmaxf(mx, d1[m][nt][e + 1] + d2[m][nt][e + 1] * LO_INV);
-            if (row2) {
-              mx = fmaxf(mx, d1[m + 1][nt][e] + d2[m + 1][nt][e] * LO_INV);
-              if (col2) mx = fmaxf(mx, d1[m + 1][nt][e + 1] + d2[m + 1][nt][e + 1] * LO_INV);
-            }
-            a.y[((p.clip * hp + (oh >> 1)) * wp + (ow >> 1)) * C + n] = mx + b;
-          }
-        }
-      } else {
-#pragma unroll
-        for (int m = 0; m < MT2; ++m) {
-          const int oh = p.h0 + wm * MT2 + m;
-          if (oh >= a.h) continue;
-          const int64_t rowbase = (p.clip * a.h + oh) * a.w;
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int ow = p.w0 + 4 * grp + i;
-            if (ow >= a.w) continue;
-            const int64_t o = (rowbase + ow) * C + n;
-            a.y[o] = d1[m][nt][i] + d2[m][nt][i] * LO_INV + b + a.x[o];
-          }
+        for (int i = 0; i < 4; ++i) {
+          if (!interior && w0 + 4 * grp + i >= a.w) continue;
+          const int64_t o = (rowbase + i) * C + n;
+          a.y[o] = d1[m][nt][i] + d2[m][nt][i] * LO_INV + b + a.x[o];
         }
       }
     }
   }
 }
 
-template <int CIN, int C, int WN, bool POOL>
+template <int CIN, int C, bool POOL>
 hipError_t launch(const ResBlkArgs& a, hipStream_t s) {
   const int total = a.n * a.tiles_h * a.tiles_w;
-  hipLaunchKernelGGL((resblk_kernel<CIN, C, WN, POOL>), dim3(total), dim3(NT), 0, s, a, total);
+  hipLaunchKernelGGL((resblk_kernel<CIN, C, POOL>), dim3(total), dim3(NT), 0, s, a);
   return hipGetLastError();
 }
 
@@ -398,8 +441,8 @@ hipError_t resblk_launch(ResBlkArgs a, int cin, int c, bool pool, hipStream_t s)
   a.tiles_h = (a.h + TH - 1) / TH;
   a.tiles_w = (a.w + TW - 1) / TW;
   if ((int64_t)a.n * a.tiles_h * a.tiles_w > 0x7fffffffLL) return hipErrorInvalidValue;
-  if (cin == 16) return launch<16, 32, 2, true>(a, s);
-  return launch<32, 32, 2, false>(a, s);
+  if (cin == 16) return launch<16, 32, true>(a, s);
+  return launch<32, 32, false>(a, s);
 }
 
 static uint16_t f16_bits(float f) {
