@@ -25,6 +25,17 @@
 #ifndef RB_EXP
 #define RB_EXP 0   // experiment switch for profiling (0 = product)
 #endif
+#if RB_EXP == 4
+// phase timestamps (s_memtime) of the first 8192 workgroups of the pool-block launch
+__device__ unsigned long long g_rb_t[8192 * 4 * 8];
+#define RB_MARK(k)                                                                        \
+  do {                                                                                    \
+    if (POOL && blockIdx.x < 8192 && lane == 0)                                           \
+      g_rb_t[(blockIdx.x * 4 + wave) * 8 + (k)] = __builtin_amdgcn_s_memtime();          \
+  } while (0)
+#else
+#define RB_MARK(k)
+#endif
 
 #include <algorithm>
 #include <cstring>
@@ -62,24 +73,38 @@ __device__ __forceinline__ void split2(f32x2 v, f16x2& h, f16x2& l) {
 
 template <int CIN, int C, bool POOL>
 struct Geo {
-  static constexpr int WN = C / 16 >= 2 ? 2 : 1;   // waves along N (16-column tiles)
+  static constexpr int WN = 1;                     // waves along N: each wave owns all C columns,
+                                                   // so every A fragment read feeds C/16 N tiles
   static constexpr int WM = 4 / WN;                // waves along M (tile rows)
   static constexpr int NTW = C / 16 / WN;          // N tiles per wave
   static constexpr int TR = TH + 3;                // t1 rows needed: image rows h0-1 .. h0+TH+1
   static constexpr int TRP = (TR + WM - 1) / WM * WM;   // computed (padded: no per-row branches)
-  static constexpr int XR = TRP + 2, XC = TW + 2, XNP = XR * XC;   // input halo rows h0-2.., cols w0-1..
-  static constexpr int LX = CIN + 8;               // halfs per staged input pixel (+16 B: banks)
-  static constexpr int LT = C + 8;                 // halfs per staged t1 pixel
-  static constexpr int XHALF = XNP * LX, THALF = TRP * TW * LT;
-  static constexpr int SM = XHALF > THALF ? XHALF : THALF;
+  // input halo rows h0-2 .. h0+TH+2 (the padded t1 row reads one row past it: finite LDS data,
+  // discarded result), cols w0-1 .. w0+TW
+  static constexpr int XR = TR + 2, XC = TW + 2, XNP = XR * XC;
+  // LDS pixel layouts.  ds_read_b128 of a 16 x 32 fragment (lanes = 16 consecutive pixels x 4
+  // 16-B k-groups) is conflict-free when the pixel stride is 32 mod 64 bytes
+  // (MI355X_MICROARCH.md LDS lane groups): 16 channels -> separate hi / lo planes of 32-B pixels;
+  // 32 channels -> hi and lo interleaved in one 160-B pixel (64 + 64 + 32 pad).
+  static constexpr int XPS = CIN == 16 ? 16 : (2 * CIN + 16 + 31) / 32 * 32 - 16;   // halfs
+  static constexpr int XLO = CIN == 16 ? XNP * 16 : CIN;     // lo offset from hi (halfs)
+  static constexpr int XREG = CIN == 16 ? 2 * XNP * 16 : XNP * XPS;
+  static constexpr int TPS = (2 * C + 16 + 31) / 32 * 32 - 16;   // t1: interleaved hi | lo | pad
+  static constexpr int TLO = C;
+  static constexpr int TREG = TRP * TW * TPS;
+  static constexpr int SM = XREG > TREG ? XREG : TREG;
   static constexpr int MT1 = TRP / WM;             // t1 rows per wave (GEMM 1)
   static constexpr int MT2 = TH / WM;              // output rows per wave (GEMM 2)
   static constexpr int KS1 = (9 * CIN + 31) / 32;  // GEMM 1 k-steps
   static constexpr int K1PAD = KS1 * 32;
   static constexpr int KS2 = 4 * C / 32;           // GEMM 2 k-steps
   static constexpr int KSC = (CIN + 31) / 32;      // shortcut (1x1) k-steps
-  static constexpr int LW2 = 4 * C + 8;            // halfs per LDS row of GEMM 2's weights
-  static constexpr int W2 = C * LW2;
+  static constexpr int LW2 = 4 * C + 16;           // halfs per LDS row of GEMM 2's weights (288 B)
+  // GEMM 2's weights live in LDS (B from L2 in GEMM 2 cost more than a third workgroup per CU
+  // bought for the 16-channel block: measured)
+  static constexpr bool W2LDS = true;
+  static constexpr int W2 = W2LDS ? C * LW2 : 0;
+  static constexpr int MINB = 2;                   // resident workgroups per CU (LDS budget)
   static constexpr int PF = 3;                     // GEMM 1 B fragments in flight (k-steps)
   static constexpr int QPP = CIN / 4;              // float4 per halo pixel
   static constexpr int MAXT = (XNP * QPP + NT - 1) / NT;
@@ -89,16 +114,14 @@ struct Geo {
 };
 
 template <int CIN, int C, bool POOL>
-__global__ void __launch_bounds__(NT, 2) resblk_kernel(ResBlkArgs a) {
+__global__ void __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(ResBlkArgs a) {
   using G = Geo<CIN, C, POOL>;
-  constexpr int XC = G::XC, LX = G::LX, LT = G::LT, MT1 = G::MT1, MT2 = G::MT2, NTW = G::NTW;
+  constexpr int XC = G::XC, XPS = G::XPS, TPS = G::TPS, MT1 = G::MT1, MT2 = G::MT2, NTW = G::NTW;
   constexpr int KS1 = G::KS1, K1PAD = G::K1PAD, KS2 = G::KS2, PF = G::PF, QPP = G::QPP;
   constexpr int MAXT = G::MAXT, WN = G::WN;
-  // [halo | t1] hi, [halo | t1] lo, GEMM 2 weights hi, lo
-  __shared__ __attribute__((aligned(16))) _Float16 smem[2 * G::SM + 2 * G::W2];
-  _Float16* const s_hi = smem;
-  _Float16* const s_lo = smem + G::SM;
-  _Float16* const s_w2h = smem + 2 * G::SM;
+  // [halo | t1] (hi and lo, layouts in Geo), then GEMM 2's weights hi, lo
+  __shared__ __attribute__((aligned(16))) _Float16 smem[G::SM + 2 * G::W2];
+  _Float16* const s_w2h = smem + G::SM;
   _Float16* const s_w2l = s_w2h + G::W2;
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -111,6 +134,7 @@ __global__ void __launch_bounds__(NT, 2) resblk_kernel(ResBlkArgs a) {
   const int th_i = tile / a.tiles_w;
   const int h0 = th_i * TH, w0 = (tile - th_i * a.tiles_w) * TW;
 
+  RB_MARK(0);
   // ---- issue the halo loads (all in flight at once) ----------------------------------------------
   const int q = tid % QPP;
   float4 pre[MAXT];
@@ -135,15 +159,52 @@ __global__ void __launch_bounds__(NT, 2) resblk_kernel(ResBlkArgs a) {
       }
     }
   }
+  // pool blocks: the Conv2D(1x1, stride 2) shortcut on the raw input is a small 3xFP16 GEMM whose M
+  // rows are ordered so that its accumulator layout equals the pooled epilogue's: tile j of this
+  // wave, element i of lane (grp, col) = pooled row wm*MT2/2 + 2j + (i >> 1), pooled column
+  // 2 grp + (i & 1), channel col.  Its operands are loaded here, beside the halo.
+  constexpr int MSC = POOL ? MT2 / 4 : 1;
+  constexpr int KSC = POOL ? G::KSC : 1;
+  float4 scx[KSC][MSC][2];
+  f16x8 scbh[KSC][NTW], scbl[KSC][NTW];
+  f32x4 e1[MSC][NTW], e2[MSC][NTW];
+  if constexpr (POOL) {
+    const int p = col;                            // this lane's A row (pooled pixel of the tile)
+    const int pr = (p & 3) >> 1, pc = 2 * (p >> 2) + (p & 1);
+    const float* xc = a.x + (int64_t)clip * a.h * a.w * CIN;
+#pragma unroll
+    for (int s = 0; s < KSC; ++s) {
+      const int ci = 32 * s + 8 * grp;
+#pragma unroll
+      for (int nt = 0; nt < NTW; ++nt) {
+        const int co = (wn * NTW + nt) * 16 + col;
+        scbh[s][nt] = *reinterpret_cast<const f16x8*>(a.wsh + co * (KSC * 32) + ci);
+        scbl[s][nt] = *reinterpret_cast<const f16x8*>(a.wsl + co * (KSC * 32) + ci);
+      }
+#pragma unroll
+      for (int j = 0; j < MSC; ++j) {
+        const int ih = h0 + 2 * (wm * (MT2 / 2) + 2 * j + pr), iw = w0 + 2 * pc;
+        scx[s][j][0] = scx[s][j][1] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (ci < CIN && ih < a.h && iw < a.w) {
+          const float* src = xc + (ih * a.w + iw) * CIN + ci;
+          scx[s][j][0] = *reinterpret_cast<const float4*>(src);
+          scx[s][j][1] = *reinterpret_cast<const float4*>(src + 4);
+        }
+      }
+    }
+  }
+  if constexpr (G::W2LDS) {
   // GEMM 2's weights -> LDS (16-B pieces; rows padded to spread the banks)
-  for (int i = tid; i < C * (4 * C / 8); i += NT) {
-    const int co = i / (4 * C / 8), k8 = i - co * (4 * C / 8);
-    *reinterpret_cast<f16x8*>(s_w2h + co * G::LW2 + 8 * k8) =
-        *reinterpret_cast<const f16x8*>(a.w2h + co * 4 * C + 8 * k8);
-    *reinterpret_cast<f16x8*>(s_w2l + co * G::LW2 + 8 * k8) =
-        *reinterpret_cast<const f16x8*>(a.w2l + co * 4 * C + 8 * k8);
+    for (int i = tid; i < C * (4 * C / 8); i += NT) {
+      const int co = i / (4 * C / 8), k8 = i - co * (4 * C / 8);
+      *reinterpret_cast<f16x8*>(s_w2h + co * G::LW2 + 8 * k8) =
+          *reinterpret_cast<const f16x8*>(a.w2h + co * 4 * C + 8 * k8);
+      *reinterpret_cast<f16x8*>(s_w2l + co * G::LW2 + 8 * k8) =
+          *reinterpret_cast<const f16x8*>(a.w2l + co * 4 * C + 8 * k8);
+    }
   }
 
+  RB_MARK(1);
   // ---- stage: BN1 + ELU once per element, split hi/lo; zero outside the image (conv padding) ----
   {
     const float4 sc4 = *reinterpret_cast<const float4*>(a.s1 + 4 * q);
@@ -164,12 +225,41 @@ __global__ void __launch_bounds__(NT, 2) resblk_kernel(ResBlkArgs a) {
       split2(v23, h23, l23);
       const f16x4 hv = {h01.x, h01.y, h23.x, h23.y};
       const f16x4 lv = {l01.x, l01.y, l23.x, l23.y};
-      *reinterpret_cast<f16x4*>(s_hi + px * LX + 4 * q) = hv;
-      *reinterpret_cast<f16x4*>(s_lo + px * LX + 4 * q) = lv;
+      *reinterpret_cast<f16x4*>(smem + px * XPS + 4 * q) = hv;
+      *reinterpret_cast<f16x4*>(smem + px * XPS + G::XLO + 4 * q) = lv;
     }
   }
   __syncthreads();
 
+  if constexpr (POOL) {
+#pragma unroll
+    for (int j = 0; j < MSC; ++j)
+#pragma unroll
+      for (int nt = 0; nt < NTW; ++nt) {
+        e1[j][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        e2[j][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+    for (int s = 0; s < KSC; ++s)
+#pragma unroll
+      for (int j = 0; j < MSC; ++j) {
+        const float4 u0 = scx[s][j][0], u1 = scx[s][j][1];
+        f16x2 h0_, l0_, h1_, l1_, h2_, l2_, h3_, l3_;
+        split2(f32x2{u0.x, u0.y}, h0_, l0_);
+        split2(f32x2{u0.z, u0.w}, h1_, l1_);
+        split2(f32x2{u1.x, u1.y}, h2_, l2_);
+        split2(f32x2{u1.z, u1.w}, h3_, l3_);
+        const f16x8 ah = {h0_.x, h0_.y, h1_.x, h1_.y, h2_.x, h2_.y, h3_.x, h3_.y};
+        const f16x8 al = {l0_.x, l0_.y, l1_.x, l1_.y, l2_.x, l2_.y, l3_.x, l3_.y};
+#pragma unroll
+        for (int nt = 0; nt < NTW; ++nt) {
+          e1[j][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, scbh[s][nt], e1[j][nt], 0, 0, 0);
+          e2[j][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, scbl[s][nt], e2[j][nt], 0, 0, 0);
+          e2[j][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, scbh[s][nt], e2[j][nt], 0, 0, 0);
+        }
+      }
+  }
+  RB_MARK(2);
   // ---- GEMM 1: t1 rows [wm * MT1, +MT1) x this wave's N tiles, K = (tap, ci) ----------------------
   f32x4 acc1[MT1][NTW], acc2[MT1][NTW];
 #pragma unroll
@@ -189,8 +279,8 @@ __global__ void __launch_bounds__(NT, 2) resblk_kernel(ResBlkArgs a) {
         bh[s][nt] = *reinterpret_cast<const f16x8*>(a.w1h + b1o + nt * 16 * K1PAD + 32 * s);
         bl[s][nt] = *reinterpret_cast<const f16x8*>(a.w1l + b1o + nt * 16 * K1PAD + 32 * s);
       }
-    const _Float16* ahb = s_hi + (wm * MT1 * XC + col) * LX;   // + m * XC * LX (immediate)
-    const _Float16* alb = s_lo + (wm * MT1 * XC + col) * LX;
+    const _Float16* ahb = smem + (wm * MT1 * XC + col) * XPS;   // + m * XC * XPS (immediate)
+    const _Float16* alb = ahb + G::XLO;
 #pragma unroll
     for (int s = 0; s < KS1; ++s) {
       const int kk = 32 * s + 8 * grp;
@@ -198,7 +288,7 @@ __global__ void __launch_bounds__(NT, 2) resblk_kernel(ResBlkArgs a) {
       const int ci = kk - tap * CIN;
       tap = tap > 8 ? 8 : tap;                 // k >= 9 * CIN: zero weights, any finite A
       const int dy = tap / 3, dx = tap - (tap / 3) * 3;
-      const int koff = (dy * XC + dx) * LX + ci;
+      const int koff = (dy * XC + dx) * XPS + ci;
       f16x8 ch[NTW], cl[NTW];
 #pragma unroll
       for (int nt = 0; nt < NTW; ++nt) {
@@ -214,8 +304,8 @@ __global__ void __launch_bounds__(NT, 2) resblk_kernel(ResBlkArgs a) {
       }
 #pragma unroll
       for (int m = 0; m < MT1; ++m) {
-        const f16x8 ah = *reinterpret_cast<const f16x8*>(ahb + koff + m * XC * LX);
-        const f16x8 al = *reinterpret_cast<const f16x8*>(alb + koff + m * XC * LX);
+        const f16x8 ah = *reinterpret_cast<const f16x8*>(ahb + koff + m * XC * XPS);
+        const f16x8 al = *reinterpret_cast<const f16x8*>(alb + koff + m * XC * XPS);
 #pragma unroll
         for (int nt = 0; nt < NTW; ++nt) {
 #if RB_EXP == 2
@@ -231,13 +321,15 @@ __global__ void __launch_bounds__(NT, 2) resblk_kernel(ResBlkArgs a) {
       __builtin_amdgcn_sched_barrier(0);   // keep the scheduler's LDS-read hoisting within a k-step
     }
   }
+  RB_MARK(3);
   __syncthreads();   // every wave is done with the input halo: its LDS now takes t1
+  RB_MARK(4);
 
   // ---- t1 -> LDS: BN2(acc + b1) + ELU; rows outside the image are the (4,1) conv's zero padding ----
   // BN2(v + b1) = acc1 * s2 + acc2 * (2^-11 s2) + (b1 s2 + t2): two v_pk_fma_f32 per pixel pair
   {
-    _Float16* const thb = s_hi + wm * MT1 * TW * LT + 4 * grp * LT;   // + (m * TW + i) * LT + n
-    _Float16* const tlb = s_lo + wm * MT1 * TW * LT + 4 * grp * LT;
+    _Float16* const thb = smem + wm * MT1 * TW * TPS + 4 * grp * TPS;   // + (m * TW + i) * TPS + n
+    _Float16* const tlb = thb + G::TLO;
 #pragma unroll
     for (int nt = 0; nt < NTW; ++nt) {
       const int n = (wn * NTW + nt) * 16 + col;
@@ -247,33 +339,32 @@ __global__ void __launch_bounds__(NT, 2) resblk_kernel(ResBlkArgs a) {
 #pragma unroll
       for (int m = 0; m < MT1; ++m) {
         const int ih = h0 - 1 + wm * MT1 + m;   // scalar
-        const bool inside = ih >= 0 && ih < a.h;
+        // branch-free (a branch per row serialises the 2 x MT1 x NTW independent chains)
+        const float rm = (ih >= 0 && ih < a.h) ? 1.0f : 0.0f;
+        const f32x2 rmask = {rm, rm};
 #pragma unroll
         for (int i = 0; i < 4; i += 2) {
-          f32x2 v = {0.f, 0.f};
 #if RB_EXP == 3
-          if (inside) v = f32x2{acc1[m][nt][i], acc2[m][nt][i + 1]};
-          thb[(m * TW + i) * LT + n] = (_Float16)v.x;
-          tlb[(m * TW + i) * LT + n] = (_Float16)v.y;
+          thb[(m * TW + i) * TPS + n] = (_Float16)(acc1[m][nt][i] * rm);
+          tlb[(m * TW + i) * TPS + n] = (_Float16)(acc2[m][nt][i + 1] * rm);
           continue;
 #endif
-          if (inside) {
-            const f32x2 x1 = {acc1[m][nt][i], acc1[m][nt][i + 1]};
-            const f32x2 x2 = {acc2[m][nt][i], acc2[m][nt][i + 1]};
-            v = elu2(x1 * s2v + (x2 * s2l + c2v));
-          }
+          const f32x2 x1 = {acc1[m][nt][i], acc1[m][nt][i + 1]};
+          const f32x2 x2 = {acc2[m][nt][i], acc2[m][nt][i + 1]};
+          const f32x2 v = elu2(x1 * s2v + (x2 * s2l + c2v)) * rmask;
           f16x2 hv, lv;
           split2(v, hv, lv);
-          thb[(m * TW + i) * LT + n] = hv.x;
-          tlb[(m * TW + i) * LT + n] = lv.x;
-          thb[(m * TW + i + 1) * LT + n] = hv.y;
-          tlb[(m * TW + i + 1) * LT + n] = lv.y;
+          thb[(m * TW + i) * TPS + n] = hv.x;
+          tlb[(m * TW + i) * TPS + n] = lv.x;
+          thb[(m * TW + i + 1) * TPS + n] = hv.y;
+          tlb[(m * TW + i + 1) * TPS + n] = lv.y;
         }
       }
     }
   }
   __syncthreads();
 
+  RB_MARK(5);
   // ---- GEMM 2: output rows [wm * MT2, +MT2), K = (dy, ci) over t1 rows r + dy --------------------
   f32x4 d1[MT2][NTW], d2[MT2][NTW];
 #pragma unroll
@@ -284,24 +375,30 @@ __global__ void __launch_bounds__(NT, 2) resblk_kernel(ResBlkArgs a) {
       d2[m][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
   {
-    const _Float16* ahb = s_hi + (wm * MT2 * TW + col) * LT;
-    const _Float16* alb = s_lo + (wm * MT2 * TW + col) * LT;
+    const _Float16* ahb = smem + (wm * MT2 * TW + col) * TPS;
+    const _Float16* alb = ahb + G::TLO;
     const int b2o = ((wn * NTW) * 16 + col) * G::LW2 + 8 * grp;
+    const int b2g = ((wn * NTW) * 16 + col) * 4 * C + 8 * grp;
 #pragma unroll
     for (int s = 0; s < KS2; ++s) {
       const int kk = 32 * s + 8 * grp;
       const int dy = kk / C, ci = kk - (kk / C) * C;
-      const int koff = dy * TW * LT + ci;
+      const int koff = dy * TW * TPS + ci;
       f16x8 gh[NTW], gl[NTW];
 #pragma unroll
       for (int nt = 0; nt < NTW; ++nt) {
-        gh[nt] = *reinterpret_cast<const f16x8*>(s_w2h + b2o + nt * 16 * G::LW2 + 32 * s);
-        gl[nt] = *reinterpret_cast<const f16x8*>(s_w2l + b2o + nt * 16 * G::LW2 + 32 * s);
+        if constexpr (G::W2LDS) {
+          gh[nt] = *reinterpret_cast<const f16x8*>(s_w2h + b2o + nt * 16 * G::LW2 + 32 * s);
+          gl[nt] = *reinterpret_cast<const f16x8*>(s_w2l + b2o + nt * 16 * G::LW2 + 32 * s);
+        } else {
+          gh[nt] = *reinterpret_cast<const f16x8*>(a.w2h + b2g + nt * 16 * 4 * C + 32 * s);
+          gl[nt] = *reinterpret_cast<const f16x8*>(a.w2l + b2g + nt * 16 * 4 * C + 32 * s);
+        }
       }
 #pragma unroll
       for (int m = 0; m < MT2; ++m) {
-        const f16x8 ah = *reinterpret_cast<const f16x8*>(ahb + koff + m * TW * LT);
-        const f16x8 al = *reinterpret_cast<const f16x8*>(alb + koff + m * TW * LT);
+        const f16x8 ah = *reinterpret_cast<const f16x8*>(ahb + koff + m * TW * TPS);
+        const f16x8 al = *reinterpret_cast<const f16x8*>(alb + koff + m * TW * TPS);
 #pragma unroll
         for (int nt = 0; nt < NTW; ++nt) {
 #if RB_EXP == 2
@@ -318,61 +415,11 @@ __global__ void __launch_bounds__(NT, 2) resblk_kernel(ResBlkArgs a) {
     }
   }
 
+  RB_MARK(6);
   // ---- epilogue ------------------------------------------------------------------------------------
   const bool interior = h0 + TH <= a.h && w0 + TW <= a.w;   // scalar: no per-element bounds checks
   if constexpr (POOL) {
-    // Conv2D(1x1, stride 2) shortcut on the raw input as a small 3xFP16 GEMM whose M rows are
-    // ordered so that its accumulator layout equals the pooled layout below: shortcut tile j of
-    // this wave, element i of lane (grp, col) = pooled row wm*MT2/2 + 2j + (i >> 1), pooled column
-    // 2 grp + (i & 1), channel col.
     constexpr int MSC = MT2 / 4;
-    f32x4 e1[MSC][NTW], e2[MSC][NTW];
-#pragma unroll
-    for (int j = 0; j < MSC; ++j)
-#pragma unroll
-      for (int nt = 0; nt < NTW; ++nt) {
-        e1[j][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-        e2[j][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-      }
-    {
-      const int p = col;                          // this lane's A row (pooled pixel of the tile)
-      const int pr = (p & 3) >> 1, pc = 2 * (p >> 2) + (p & 1);
-      const float* xc = a.x + (int64_t)clip * a.h * a.w * CIN;
-#pragma unroll
-      for (int s = 0; s < G::KSC; ++s) {
-        const int ci = 32 * s + 8 * grp;
-        f16x8 bh[NTW], bl[NTW];
-#pragma unroll
-        for (int nt = 0; nt < NTW; ++nt) {
-          const int co = (wn * NTW + nt) * 16 + col;
-          bh[nt] = *reinterpret_cast<const f16x8*>(a.wsh + co * (G::KSC * 32) + ci);
-          bl[nt] = *reinterpret_cast<const f16x8*>(a.wsl + co * (G::KSC * 32) + ci);
-        }
-#pragma unroll
-        for (int j = 0; j < MSC; ++j) {
-          const int ih = h0 + 2 * (wm * (MT2 / 2) + 2 * j + pr), iw = w0 + 2 * pc;
-          float4 u0 = make_float4(0.f, 0.f, 0.f, 0.f), u1 = u0;
-          if (ci < CIN && ih < a.h && iw < a.w) {
-            const float* src = xc + (ih * a.w + iw) * CIN + ci;
-            u0 = *reinterpret_cast<const float4*>(src);
-            u1 = *reinterpret_cast<const float4*>(src + 4);
-          }
-          f16x2 h0_, l0_, h1_, l1_, h2_, l2_, h3_, l3_;
-          split2(f32x2{u0.x, u0.y}, h0_, l0_);
-          split2(f32x2{u0.z, u0.w}, h1_, l1_);
-          split2(f32x2{u1.x, u1.y}, h2_, l2_);
-          split2(f32x2{u1.z, u1.w}, h3_, l3_);
-          const f16x8 ah = {h0_.x, h0_.y, h1_.x, h1_.y, h2_.x, h2_.y, h3_.x, h3_.y};
-          const f16x8 al = {l0_.x, l0_.y, l1_.x, l1_.y, l2_.x, l2_.y, l3_.x, l3_.y};
-#pragma unroll
-          for (int nt = 0; nt < NTW; ++nt) {
-            e1[j][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh[nt], e1[j][nt], 0, 0, 0);
-            e2[j][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl[nt], e2[j][nt], 0, 0, 0);
-            e2[j][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh[nt], e2[j][nt], 0, 0, 0);
-          }
-        }
-      }
-    }
     const int hp = (a.h + 1) >> 1, wp = (a.w + 1) >> 1;
 #pragma unroll
     for (int nt = 0; nt < NTW; ++nt) {
@@ -418,6 +465,7 @@ __global__ void __launch_bounds__(NT, 2) resblk_kernel(ResBlkArgs a) {
       }
     }
   }
+  RB_MARK(7);
 }
 
 template <int CIN, int C, bool POOL>
@@ -428,6 +476,12 @@ hipError_t launch(const ResBlkArgs& a, hipStream_t s) {
 }
 
 }  // namespace
+
+#if RB_EXP == 4
+extern "C" int mmla_debug_resblk_times(unsigned long long* host) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_rb_t), sizeof(g_rb_t));
+}
+#endif
 
 int resblk_k1pad(int cin) { return (9 * cin + 31) / 32 * 32; }
 
