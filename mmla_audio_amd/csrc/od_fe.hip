@@ -8,11 +8,12 @@
 //   zero_crossing_rate(400, 160)        :100  (edge padding, signbit crossings)
 //   generate_zcr_image + imsave + decode_png   :133-151, record_on_pc.py:156-158
 //
-// Layout / schedule (one workgroup = one clip, 512 threads = 8 waves, 2 per SIMD):
-//   LDS: pcm int16[24000] (48 000 B) + STFT scratch (2 x FT*225 complex) + S f32[128][151]
-//        (77 312 B) -> ~154 KB, one workgroup per CU.
-//   The clip's normalisation needs the clip-global max/min of S, so all 151 frames of mel power
-//   stay on chip and the outputs are written once, coalesced, after a block reduction.
+// Layout / schedule: one workgroup = one wave = one clip (no block barriers beyond the wave's own),
+// ~16 KB of LDS, so ~10 clips are in flight per CU.  Frames go in groups of F = 5 (125 / 225 / 225 /
+// 640 lane tasks per pass, 88-100 % of the lanes busy): the group's reflect-padded 1040-sample
+// window is staged in LDS, the three DFT passes run in one LDS buffer, and the mel power goes to an
+// HBM-backed scratch (the norm output itself when it is requested).  The clip's normalisation needs
+// the clip-global max/min, so the scratch is re-read (L2/MALL-resident) once the last group is done.
 // 400-point real DFT per frame, factored n = 25*n1 + n2, k = k1 + 16*k2:
 //   pass 1 (25 tasks/frame): real 16-point DFT over n1 (via a complex 8-point FFT), k1 = 0..8,
 //                            times W400^(n2*k1)
@@ -33,25 +34,20 @@ constexpr int HOP = 160;
 constexpr int CLIP = 24000;
 constexpr int NF = 151;
 constexpr int NMEL = 128;
-constexpr int FT = 8;            // frames per STFT tile
-constexpr int NT = 512;          // threads per workgroup
-constexpr int NCHUNK = 305;      // ZCR: 80-sample chunks of the 24400-sample edge-padded signal
+constexpr int F = 5;             // frames per group: 25 F, 45 F, 128 F lane tasks per pass
+constexpr int NG = (NF + F - 1) / F;
+constexpr int WIN = (F - 1) * HOP + N_FFT;   // samples behind one group of frames
+constexpr int NT = 64;           // one wave per workgroup (= per clip): no block barriers
 
-struct Smem {
-  int16_t pcm[CLIP];
-  cf t1[FT][9][25];              // pass-1 output  [frame][k1][n2]
-  cf t2[FT][9][25];              // pass-2 output  [frame][k1][c*5+b]; pass 3 writes power into t1
-  float s[NMEL][NF];             // mel power
-  int cc[NCHUNK + 3];            // ZCR chunk counts
-  int zc[NF];                    // ZCR counts per frame
-  float red[2][NT / 64];
+struct Smem {                    // 15.9 KB: ~10 clips in flight per CU
+  int16_t win[WIN + 16];         // reflect-padded window of the group, base = 160 f0 - 200
+  cf t[F][9][25];                // pass 1 output, transformed in place by pass 2a
+  float pw[F][216];              // power spectrum (bins 0..200; 201.. stay 0 for the 10-tap mel dot)
+  int zc[NF + 1];                // ZCR counts of the clip
+  float hann[N_FFT];             // tables the lanes index per task (LDS, not L2 latency)
+  float w400[9][25][2];
+  float w25[5][5][2];
 };
-
-MMLA_DEV float sample(const Smem& sm, int i) {   // reflect padding of the 24000-sample clip
-  i = i < 0 ? -i : i;
-  i = i >= CLIP ? 2 * (CLIP - 1) - i : i;
-  return (float)sm.pcm[i] * (1.0f / 32768.0f);
-}
 
 MMLA_DEV void fft4(cf& a0, cf& a1, cf& a2, cf& a3) {
   cf s02 = cadd(a0, a2), d02 = csub(a0, a2), s13 = cadd(a1, a3), d13 = csub(a1, a3);
@@ -98,64 +94,129 @@ MMLA_DEV void dft5(cf x0, cf x1, cf x2, cf x3, cf x4, cf y[5]) {
 }
 
 __global__ void __launch_bounds__(NT) od_fe_kernel(OdFeArgs a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-  Smem& sm = *reinterpret_cast<Smem*>(smem_raw);
+  __shared__ __attribute__((aligned(16))) Smem sm;
   const OdFeTables& tb = *a.tables;
-  const int tid = threadIdx.x;
+  const int lane = threadIdx.x;
   const int64_t clip = blockIdx.x;
 
-  // ---- stage the clip (first 24000 samples, zero-padded) into LDS -------------------------------
   int len = a.lens ? a.lens[clip] : a.clip_len;
   len = len < 0 ? 0 : (len > CLIP ? CLIP : len);
   const int16_t* src = a.pcm + clip * a.clip_stride;
-  if (len == CLIP && ((reinterpret_cast<uintptr_t>(src) & 15) == 0)) {
-    const uint4* s4 = reinterpret_cast<const uint4*>(src);
-    uint4* d4 = reinterpret_cast<uint4*>(sm.pcm);
-    for (int i = tid; i < CLIP / 8; i += NT) d4[i] = s4[i];
-  } else {
-    for (int i = tid; i < CLIP; i += NT) sm.pcm[i] = i < len ? src[i] : (int16_t)0;
-  }
-  __syncthreads();
+  // mel power of the whole clip goes to HBM-backed scratch (the norm output itself when requested:
+  // normalised in place), L2/MALL-resident until the normalisation pass below re-reads it
+  float* scr = (a.norm ? a.norm : a.scratch) + clip * (NMEL * NF);
+  // edge padding of the ZCR: samples before / after the clip repeat its first / last sample
+  const int sg_first = (len > 0 ? src[0] : (int16_t)0) < 0;
+  const int sg_last = (CLIP - 1 < len ? src[CLIP - 1] : (int16_t)0) < 0;
 
-  // ---- zero-crossing counts (edge-padded signal, padded index p <-> clip index clamp(p-200)) ----
-  for (int q = tid; q < NCHUNK; q += NT) {
-    int cnt = 0;
-    int p0 = q * 80;
-    int prev = p0 == 0 ? -1 : sm.pcm[min(max(p0 - 1 - 200, 0), CLIP - 1)] < 0;
-    for (int j = 0; j < 80; ++j) {
-      int p = p0 + j;
-      int sgn = sm.pcm[min(max(p - 200, 0), CLIP - 1)] < 0;
-      cnt += (prev >= 0) & (sgn != prev);
-      prev = sgn;
+  // the window of group g + 1 is loaded into registers (3 x 16 B per lane) while group g computes;
+  // groups whose window leaves [0, len) take the scalar reflect / zero-fill path instead
+  constexpr int WCH = WIN / 8;                       // 16-B chunks per window (130)
+  constexpr int WPL = (WCH + NT - 1) / NT;           // chunks per lane (3)
+  const bool vec_ok = ((reinterpret_cast<uintptr_t>(src) & 15) == 0);
+  auto fast = [&](int g_) {
+    const int b_ = HOP * g_ * F - N_FFT / 2;
+    return vec_ok && b_ >= 0 && b_ + WIN <= len;
+  };
+  uint4 nxt[WPL];
+  auto prefetch = [&](int g_) {
+    const uint4* s4 = reinterpret_cast<const uint4*>(src + HOP * g_ * F - N_FFT / 2);
+#pragma unroll
+    for (int j = 0; j < WPL; ++j) {
+      const int ch = lane + NT * j;
+      if (ch < WCH) nxt[j] = s4[ch];
     }
-    sm.cc[q] = cnt;
-  }
-  __syncthreads();
-  for (int f = tid; f < NF; f += NT) {
-    // frame f covers padded [160 f, 160 f + 400): chunks 2f .. 2f+4, minus the change at 160 f
-    int c = sm.cc[2 * f] + sm.cc[2 * f + 1] + sm.cc[2 * f + 2] + sm.cc[2 * f + 3] + sm.cc[2 * f + 4];
-    int p = HOP * f;
-    if (p > 0) {
-      int s0 = sm.pcm[min(max(p - 1 - 200, 0), CLIP - 1)] < 0;
-      int s1 = sm.pcm[min(max(p - 200, 0), CLIP - 1)] < 0;
-      c -= (s0 != s1);
-    }
-    sm.zc[f] = c;
+  };
+  if (fast(0)) prefetch(0);
+
+  for (int i = lane; i < N_FFT; i += NT) sm.hann[i] = tb.hann[i];
+  for (int i = lane; i < 9 * 25 * 2; i += NT) (&sm.w400[0][0][0])[i] = (&tb.w400[0][0][0])[i];
+  for (int i = lane; i < 5 * 5 * 2; i += NT) (&sm.w25[0][0][0])[i] = (&tb.w25[0][0][0])[i];
+  for (int i = lane; i < F * 216; i += NT) (&sm.pw[0][0])[i] = 0.0f;
+  // this lane's two mel bands: start bin and 10 weights (zero past the band's non-zeros)
+  int mst[NMEL / NT];
+  float mw[NMEL / NT][10];
+#pragma unroll
+  for (int mh = 0; mh < NMEL / NT; ++mh) {
+    const int m = lane + NT * mh;
+    mst[mh] = tb.mel_start[m];
+#pragma unroll
+    for (int j = 0; j < 10; ++j) mw[mh][j] = tb.mel_w[m][j];
   }
 
-  // ---- STFT -> power -> mel, FT frames per tile ---------------------------------------------------
   float smax = 0.0f, smin = INFINITY;
-  for (int f0 = 0; f0 < NF; f0 += FT) {
-    const int nfr = min(FT, NF - f0);
-    // pass 1: real 16-point DFT over n1 of x[25 n1 + n2] * hann
-    for (int task = tid; task < nfr * 25; task += NT) {
+  for (int g = 0; g < NG; ++g) {
+    const int f0 = g * F;
+    const int base = HOP * f0 - N_FFT / 2;
+    __syncthreads();   // the previous group is done with win / t / pw
+    // ---- window: reflect padding for the STFT (centre=True, pad_mode='reflect') ----------------
+    if (fast(g)) {
+#pragma unroll
+      for (int j = 0; j < WPL; ++j) {
+        const int ch = lane + NT * j;
+        if (ch < WCH) reinterpret_cast<uint4*>(sm.win)[ch] = nxt[j];
+      }
+    } else {
+      for (int w = lane; w < WIN; w += NT) {
+        int i = base + w;
+        i = i < 0 ? -i : i;
+        i = i >= CLIP ? 2 * (CLIP - 1) - i : i;
+        sm.win[w] = i < len ? src[i] : (int16_t)0;
+      }
+    }
+    if (g + 1 < NG && fast(g + 1)) prefetch(g + 1);
+    __syncthreads();
+    // ---- zero crossings of the group's frames (edge padding; transitions at padded positions
+    //      160 f + 1 .. 160 f + 399, signbit semantics) ---------------------------------------------
+    // lane l < 52 counts the transitions (w - 1, w) at window positions w = 20 l .. 20 l + 19; frame f
+    // covers lanes 8 f .. 8 f + 19 minus position 160 f (its first transition is outside the frame).
+    // Windows that touch the clip edge (edge vs reflect padding differ there) index per position.
+    {
+      constexpr int ZCH = 20, ZL = WIN / ZCH;      // 52 lanes
+      static_assert(WIN % ZCH == 0 && HOP % ZCH == 0 && N_FFT % ZCH == 0, "ZCR chunking");
+      const bool interior = base >= 0 && base + WIN <= CLIP;
+      auto sgn = [&](int w) {
+        const int i = base + w;
+        return i < 0 ? sg_first : (i >= CLIP ? sg_last : (int)(sm.win[w] < 0));
+      };
+      int cl = 0, first = 0;
+      if (lane < ZL) {
+        const int w0 = ZCH * lane;
+        int prev = w0 == 0 ? -1 : (interior ? (int)(sm.win[w0 - 1] < 0) : sgn(w0 - 1));
+#pragma unroll
+        for (int j = 0; j < ZCH; ++j) {
+          const int cur = interior ? (int)(sm.win[w0 + j] < 0) : sgn(w0 + j);
+          const int x = (prev >= 0) & (cur != prev);
+          cl += x;
+          if (j == 0) first = x;
+          prev = cur;
+        }
+      }
+      int* scan = reinterpret_cast<int*>(sm.t);  // t is free until pass 1 writes it
+      scan[lane] = cl;
+      scan[NT + lane] = first;
+      __syncthreads();
+      if (lane < F && f0 + lane < NF) {
+        int c = 0;
+#pragma unroll
+        for (int l = 0; l < 20; ++l) c += scan[8 * lane + l];
+        sm.zc[f0 + lane] = c - scan[NT + 8 * lane];
+      }
+      __syncthreads();
+    }
+    // ---- pass 1: real 16-point DFT over n1 of x[25 n1 + n2] * hann, times W400^(n2 k1) ----------
+#pragma unroll
+    for (int r = 0; r < (F * 25 + NT - 1) / NT; ++r) {
+      const int task = lane + NT * r;
+      if (task >= F * 25) break;
       const int f = task / 25, n2 = task - f * 25;
-      const int base = HOP * (f0 + f) - N_FFT / 2;
+      const int16_t* x = sm.win + HOP * f;
       cf z[8];
 #pragma unroll
       for (int m = 0; m < 8; ++m) {
         const int ne = 25 * (2 * m) + n2, no = 25 * (2 * m + 1) + n2;
-        z[m] = {sample(sm, base + ne) * tb.hann[ne], sample(sm, base + no) * tb.hann[no]};
+        z[m] = {(float)x[ne] * (1.0f / 32768.0f) * sm.hann[ne],
+                (float)x[no] * (1.0f / 32768.0f) * sm.hann[no]};
       }
       fft8(z);
 #pragma unroll
@@ -166,71 +227,69 @@ __global__ void __launch_bounds__(NT) od_fe_kernel(OdFeArgs a) {
         cf o = {0.5f * d.y, -0.5f * d.x};                     // d / (2i)
         cf w16 = {tb.w16[k][0], tb.w16[k][1]};
         cf y = cadd(e, cmul(w16, o));
-        cf tw = {tb.w400[k][n2][0], tb.w400[k][n2][1]};
-        sm.t1[f][k][n2] = cmul(y, tw);
+        cf tw = {sm.w400[k][n2][0], sm.w400[k][n2][1]};
+        sm.t[f][k][n2] = cmul(y, tw);
       }
     }
     __syncthreads();
-    // pass 2: DFT-5 over a of t1[k1][5a + b], times W25^(b c)
-    for (int task = tid; task < nfr * 45; task += NT) {
+    // ---- pass 2a: DFT-5 over a of t[k1][5a + b], times W25^(b c), in place at t[k1][5c + b] -------
+#pragma unroll
+    for (int rr = 0; rr < (F * 45 + NT - 1) / NT; ++rr) {
+      const int task = lane + NT * rr;
+      if (task >= F * 45) break;
       const int f = task / 45, r = task - f * 45, k1 = r / 5, b = r - k1 * 5;
       cf y[5];
-      dft5(sm.t1[f][k1][b], sm.t1[f][k1][5 + b], sm.t1[f][k1][10 + b], sm.t1[f][k1][15 + b],
-           sm.t1[f][k1][20 + b], y);
+      dft5(sm.t[f][k1][b], sm.t[f][k1][5 + b], sm.t[f][k1][10 + b], sm.t[f][k1][15 + b],
+           sm.t[f][k1][20 + b], y);
 #pragma unroll
       for (int c = 0; c < 5; ++c) {
-        cf tw = {tb.w25[b][c][0], tb.w25[b][c][1]};
-        sm.t2[f][k1][c * 5 + b] = cmul(y[c], tw);
+        cf tw = {sm.w25[b][c][0], sm.w25[b][c][1]};
+        sm.t[f][k1][c * 5 + b] = cmul(y[c], tw);
       }
     }
     __syncthreads();
-    // pass 3: DFT-5 over b -> X[k1 + 16 (c + 5 d)] -> power into t1 (reused as float[FT][201+])
-    float* pw = reinterpret_cast<float*>(&sm.t1[0][0][0]);
-    for (int task = tid; task < nfr * 45; task += NT) {
+    // ---- pass 2b: DFT-5 over b -> X[k1 + 16 (c + 5 d)] -> power; bins > 200 fold onto 400 - k ---
+#pragma unroll
+    for (int rr = 0; rr < (F * 45 + NT - 1) / NT; ++rr) {
+      const int task = lane + NT * rr;
+      if (task >= F * 45) break;
       const int f = task / 45, r = task - f * 45, k1 = r / 5, c = r - k1 * 5;
       cf y[5];
-      dft5(sm.t2[f][k1][c * 5 + 0], sm.t2[f][k1][c * 5 + 1], sm.t2[f][k1][c * 5 + 2],
-           sm.t2[f][k1][c * 5 + 3], sm.t2[f][k1][c * 5 + 4], y);
+      dft5(sm.t[f][k1][c * 5 + 0], sm.t[f][k1][c * 5 + 1], sm.t[f][k1][c * 5 + 2],
+           sm.t[f][k1][c * 5 + 3], sm.t[f][k1][c * 5 + 4], y);
 #pragma unroll
       for (int d = 0; d < 5; ++d) {
         const int bin = k1 + 16 * (c + 5 * d);
         const float p = fmaf(y[d].x, y[d].x, y[d].y * y[d].y);
         if (bin <= 200)
-          pw[f * 208 + bin] = p;
+          sm.pw[f][bin] = p;
         else if (k1 >= 1 && k1 <= 7)
-          pw[f * 208 + (N_FFT - bin)] = p;
+          sm.pw[f][N_FFT - bin] = p;
       }
     }
     __syncthreads();
-    // mel: S[m][f] = sum_j w[m][j] * P[f][start_m + j]
-    for (int task = tid; task < nfr * NMEL; task += NT) {
-      const int f = task / NMEL, m = task - f * NMEL;
-      const int st = tb.mel_start[m], cnt = tb.mel_cnt[m];
-      const float* p = pw + f * 208 + st;
-      float acc = 0.0f;
-      for (int j = 0; j < cnt; ++j) acc = fmaf(tb.mel_w[m][j], p[j], acc);
-      sm.s[m][f0 + f] = acc;
-      smax = fmaxf(smax, acc);
-      smin = fminf(smin, acc);
+    // ---- mel: S[m][f] = sum_j w[m][j] * P[f][start_m + j] -> scratch ---------------------------------
+#pragma unroll
+    for (int mh = 0; mh < NMEL / NT; ++mh) {
+      const int m = lane + NT * mh;
+#pragma unroll
+      for (int f = 0; f < F; ++f) {
+        if (f0 + f >= NF) break;
+        const float* p = &sm.pw[f][mst[mh]];
+        float acc = 0.0f;   // the band's non-zeros in order, then exact zero terms: same result
+#pragma unroll
+        for (int j = 0; j < 10; ++j) acc = fmaf(mw[mh][j], p[j], acc);
+        scr[m * NF + f0 + f] = acc;
+        smax = fmaxf(smax, acc);
+        smin = fminf(smin, acc);
+      }
     }
-    __syncthreads();
   }
-
-  // ---- clip-global max / min of the mel power -----------------------------------------------------
+  // ---- clip max / min of the mel power (one wave: shuffles only) ----------------------------------
   smax = wave_max(smax);
   smin = wave_min(smin);
-  if ((tid & 63) == 0) {
-    sm.red[0][tid >> 6] = smax;
-    sm.red[1][tid >> 6] = smin;
-  }
+  __threadfence();   // the scratch stores are visible to the re-reads below (other lanes)
   __syncthreads();
-  smax = sm.red[0][0];
-  smin = sm.red[1][0];
-#pragma unroll
-  for (int w = 1; w < NT / 64; ++w) {
-    smax = fmaxf(smax, sm.red[0][w]);
-    smin = fminf(smin, sm.red[1][w]);
-  }
 
   // power_to_db(ref=np.max, amin=1e-10, top_db=80) with numpy-1.21 dtypes, then normalize_matrix.
   // log10 is monotone, so max/min of the dB matrix are the dB of max/min S.  Each numpy op rounds
@@ -245,40 +304,54 @@ __global__ void __launch_bounds__(NT) od_fe_kernel(OdFeArgs a) {
   const float diff = d_max - d_min;
 
   float* db_out = a.db ? a.db + clip * (NMEL * NF) : nullptr;
-  float* nm_out = a.norm ? a.norm + clip * (NMEL * NF) : nullptr;
-  for (int e = tid; e < NMEL * NF; e += NT) {
-    const int m = e / NF, t = e - m * NF;
-    float d = 10.0f * log10f(fmaxf(amin, sm.s[m][t])) - ref_db;
-    d = fmaxf(d, thr);
-    const float nv = (d - d_min) / diff;
-    if (db_out) db_out[e] = d;
-    if (nm_out) nm_out[e] = nv;
-    sm.s[m][t] = nv;   // keep the normalised value for the image
+  const bool normed = db_out || a.norm;
+  if (normed) {
+    for (int e = lane; e < NMEL * NF; e += NT) {
+      float d = 10.0f * log10f(fmaxf(amin, scr[e])) - ref_db;
+      d = fmaxf(d, thr);
+      const float nv = (d - d_min) / diff;
+      if (db_out) db_out[e] = d;
+      scr[e] = nv;   // the norm output (or scratch the image reads)
+    }
   }
   if (a.zcr) {
-    for (int f = tid; f < NF; f += NT) a.zcr[clip * NF + f] = (float)sm.zc[f] * (1.0f / 400.0f);
+    for (int f = lane; f < NF; f += NT) a.zcr[clip * NF + f] = (float)sm.zc[f] * (1.0f / 400.0f);
   }
   if (a.img) {
-    __syncthreads();
+    if (normed) {
+      __threadfence();
+      __syncthreads();
+    }
     // img[h][w][ch]: R = trunc(255 * zcr[w]) (float64), G = B = trunc(255 * (1 - norm[127-h][w]))
-    // (float64: numpy-1.21 '1 - np.float32' promotes); NaN -> 0.
+    // (float64: numpy-1.21 '1 - np.float32' promotes); NaN -> 0.  One lane = 4 pixels = 3 words.
+    uint8_t* rb = reinterpret_cast<uint8_t*>(sm.pw);   // R byte per column (pw is free now)
+    for (int w = lane; w < NF; w += NT) {
+      const double v = ((double)sm.zc[w] / 400.0) * 255.0;
+      rb[w] = (uint8_t)(int)v;
+    }
+    __syncthreads();
     uint32_t* out = reinterpret_cast<uint32_t*>(a.img + clip * (NMEL * NF * 3));
-    for (int wd = tid; wd < NMEL * NF * 3 / 4; wd += NT) {
-      uint32_t word = 0;
+    for (int qd = lane; qd < NMEL * NF / 4; qd += NT) {
+      uint32_t by[12];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int q = wd * 4 + j;
-        const int px = q / 3, ch = q - px * 3;
+        const int px = 4 * qd + j;
         const int h = px / NF, w = px - h * NF;
-        double v;
-        if (ch == 0)
-          v = ((double)sm.zc[w] / 400.0) * 255.0;
-        else
-          v = (1.0 - (double)sm.s[NMEL - 1 - h][w]) * 255.0;
-        const uint32_t byte = (v >= 0.0) ? (uint32_t)(int)v : 0u;   // NaN fails v >= 0
-        word |= (byte & 255u) << (8 * j);
+        float nv = scr[(NMEL - 1 - h) * NF + w];
+        if (!normed) {
+          float d = 10.0f * log10f(fmaxf(amin, nv)) - ref_db;
+          d = fmaxf(d, thr);
+          nv = (d - d_min) / diff;
+        }
+        const double v = (1.0 - (double)nv) * 255.0;
+        const uint32_t gb = (v >= 0.0) ? ((uint32_t)(int)v & 255u) : 0u;   // NaN fails v >= 0
+        by[3 * j] = rb[w];
+        by[3 * j + 1] = gb;
+        by[3 * j + 2] = gb;
       }
-      out[wd] = word;
+#pragma unroll
+      for (int k = 0; k < 3; ++k)
+        out[3 * qd + k] = by[4 * k] | (by[4 * k + 1] << 8) | (by[4 * k + 2] << 16) | (by[4 * k + 3] << 24);
     }
   }
   }
@@ -290,15 +363,8 @@ size_t od_fe_smem_bytes() { return sizeof(Smem); }
 
 hipError_t od_fe_launch(const OdFeArgs& a, int64_t n_clips, hipStream_t stream) {
   if (n_clips <= 0) return hipSuccess;
-  const size_t smem = sizeof(Smem);
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(od_fe_kernel),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-    if (e != hipSuccess) return e;
-    attr_set = true;
-  }
-  hipLaunchKernelGGL(od_fe_kernel, dim3((unsigned)n_clips), dim3(NT), smem, stream, a);
+  if (!a.norm && !a.scratch) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(od_fe_kernel, dim3((unsigned)n_clips), dim3(NT), 0, stream, a);
   return hipGetLastError();
 }
 
