@@ -22,7 +22,7 @@
 namespace {
 
 constexpr int NT = 256;
-constexpr int FT = 16;
+constexpr int FT = 12;          // frames per tile: LDS 64 KB -> 2 workgroups per CU
 constexpr int HALO = 4;              // delta-delta reach in frames
 constexpr int OUTF = 256;
 constexpr int NL = OUTF + 2 * HALO;  // local frames per window: [frame0 - 4, frame0 + 260)
@@ -30,8 +30,8 @@ constexpr int NL = OUTF + 2 * HALO;  // local frames per window: [frame0 - 4, fr
 struct Smem {
   cd buf[FT][256];      // pass A output -> (in place) Z -> (in place) power spectrum [f][258]
   double lfe[FT][28];   // log filterbank energies + log energy
-  double feat[NL][13];
-  double dlt[NL][13];
+  float feat[NL][13];   // cepstra (float64 math, stored float32: the deltas' inputs); the deltas
+                        // themselves are recomputed per output element instead of staged
 };
 
 template <typename C>
@@ -65,7 +65,7 @@ MMLA_DEV double pre(const int16_t* x, int64_t i, int64_t len) {
   return i == 0 ? (double)x[0] : (double)x[i] - 0.97 * (double)x[i - 1];
 }
 
-__global__ void __launch_bounds__(NT) si_fe_kernel(SiFeArgs a) {
+__global__ void __launch_bounds__(NT, 2) si_fe_kernel(SiFeArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   Smem& sm = *reinterpret_cast<Smem*>(smem_raw);
   const SiFeTables& tb = *a.tables;
@@ -159,8 +159,10 @@ __global__ void __launch_bounds__(NT) si_fe_kernel(SiFeArgs a) {
           const cd o = {0.5 * d.y, -0.5 * d.x};
           const cd w = {tb.w512[k][0], tb.w512[k][1]};
           const cd X = cadd(e, cmul(w, o));
-          const double mag = hypot(X.x, X.y);   // numpy.absolute
-          pv[r] = (mag * mag) * (1.0 / 512.0);  // 1/NFFT * square(mag)
+          // numpy: square(absolute(X)) / 512 with absolute = hypot; x^2 + y^2 differs from
+          // hypot^2 by an ulp (no fp64 sqrt/div on the hot path)
+          const double mag2 = X.x * X.x + X.y * X.y;
+          pv[r] = mag2 * (1.0 / 512.0);
         }
       }
       __syncthreads();
@@ -199,7 +201,7 @@ __global__ void __launch_bounds__(NT) si_fe_kernel(SiFeArgs a) {
         v = 0.0;
         for (int j = 0; j < 26; ++j) v += sm.lfe[f][j] * tb.dct[c][j];
       }
-      sm.feat[lf0 + t0 + f][c] = v;
+      sm.feat[lf0 + t0 + f][c] = (float)v;
     }
     __syncthreads();
   }
@@ -210,28 +212,27 @@ __global__ void __launch_bounds__(NT) si_fe_kernel(SiFeArgs a) {
     g = g < 0 ? 0 : (g > T - 1 ? T - 1 : g);
     return (int)(g - (frame0 - HALO));
   };
-  for (int e = tid; e < (OUTF + 2 * 2) * 13; e += NT) {   // delta rows g in [frame0-2, frame0+258)
-    const int r = e / 13, c = e - r * 13;
-    const int64_t g = frame0 - 2 + r;
-    if (g < 0 || g > T - 1) continue;
-    const double v = -2.0 * sm.feat[loc(g - 2)][c] - 1.0 * sm.feat[loc(g - 1)][c] +
-                     1.0 * sm.feat[loc(g + 1)][c] + 2.0 * sm.feat[loc(g + 2)][c];
-    sm.dlt[loc(g)][c] = v / 10.0;
-  }
-  __syncthreads();
+  // delta of feat column c at global frame g (g clamped by the caller)
+  auto dfe = [&](int64_t g, int c) {
+    const double v = -2.0 * (double)sm.feat[loc(g - 2)][c] - 1.0 * (double)sm.feat[loc(g - 1)][c] +
+                     1.0 * (double)sm.feat[loc(g + 1)][c] + 2.0 * (double)sm.feat[loc(g + 2)][c];
+    return v / 10.0;
+  };
+  auto clampg = [&](int64_t g) { return g < 0 ? (int64_t)0 : (g > T - 1 ? T - 1 : g); };
   for (int e = tid; e < OUTF * 39; e += NT) {
     const int t = e / 39, c = e - t * 39;
     const int64_t g = frame0 + t;
     float v = 0.0f;
     if (g < T) {
       if (c < 13) {
-        v = (float)sm.feat[loc(g)][c];
+        v = sm.feat[loc(g)][c];
       } else if (c < 26) {
-        v = (float)sm.dlt[loc(g)][c - 13];
+        v = (float)dfe(g, c - 13);
       } else {
+        // delta of the delta sequence, itself edge-padded at the true ends
         const int cc = c - 26;
-        const double d = -2.0 * sm.dlt[loc(g - 2)][cc] - 1.0 * sm.dlt[loc(g - 1)][cc] +
-                         1.0 * sm.dlt[loc(g + 1)][cc] + 2.0 * sm.dlt[loc(g + 2)][cc];
+        const double d = -2.0 * dfe(clampg(g - 2), cc) - 1.0 * dfe(clampg(g - 1), cc) +
+                         1.0 * dfe(clampg(g + 1), cc) + 2.0 * dfe(clampg(g + 2), cc);
         v = (float)(d / 10.0);
       }
     }
