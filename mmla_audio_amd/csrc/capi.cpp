@@ -471,10 +471,15 @@ int run_od_net(mmla_ctx* c, const uint8_t* img_u8, const float* img_f32, int64_t
   float* X = static_cast<float*>(px);
   float* T1 = static_cast<float*>(pt1);
   float* T2 = static_cast<float*>(pt2);
-  // Conv2D(16, 1x1) on the PNG image (overlap_detector_temp.py:282)
-  LAUNCH(c, MMLA_STAGE_GLUE, 2.0 * n * OD_PIX * 3 * 16,
-         od_stem_launch(img_u8, img_f32, n * OD_PIX, W.stem.cout_pad, W.stem.wt, W.stem.bias, X,
-                        c->stream));
+  // Conv2D(16, 1x1) on the PNG image (overlap_detector_temp.py:282): computed inside block 1's
+  // staging when block 1 runs fused (resblk.hip STEM), else its own launch
+  const bool fuse_stem = c->precision == MMLA_PREC_F16X3 && stop != 0 && W.blk[0].c3.fh &&
+                         W.blk[0].c4.fh && W.blk[0].sc.fh &&
+                         resblk_supported(W.blk[0].c3.cin, W.blk[0].c3.cout, POOL[0]);
+  if (!fuse_stem)
+    LAUNCH(c, MMLA_STAGE_GLUE, 2.0 * n * OD_PIX * 3 * 16,
+           od_stem_launch(img_u8, img_f32, n * OD_PIX, W.stem.cout_pad, W.stem.wt, W.stem.bias, X,
+                          c->stream));
   int h = OD_H, w = OD_W;
   if (stop == 0) {
     *tap = X;
@@ -505,10 +510,19 @@ int run_od_net(mmla_ctx* c, const uint8_t* img_u8, const float* img_f32, int64_t
         r.bs = B.sc.bias;
       }
       r.y = T1;
+      if (b == 0 && fuse_stem) {
+        r.x = nullptr;
+        r.img8 = img_u8;
+        r.imgf = img_u8 ? nullptr : img_f32;
+        r.wst = W.stem.wt;
+        r.bst = W.stem.bias;
+        r.ldst = W.stem.cout_pad;
+      }
       r.n = (int)n;
       r.h = h;
       r.w = w;
       LAUNCH(c, MMLA_STAGE_CONV,
+             (b == 0 && fuse_stem ? 2.0 * n * h * w * 3 * 16 : 0.0) +
              2.0 * n * h * w * (9.0 * B.c3.cin * B.c3.cout + 4.0 * B.c4.cin * B.c4.cout) +
                  (POOL[b] ? 2.0 * n * ((h + 1) / 2) * ((w + 1) / 2) * B.sc.cin * B.sc.cout : 0.0),
              resblk_launch(r, B.c3.cin, B.c3.cout, POOL[b], c->stream));

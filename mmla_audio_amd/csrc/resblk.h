@@ -18,6 +18,11 @@ struct ResBlkArgs {
   const uint16_t* wsh;     // pool blocks: Conv2D(1x1, stride 2) shortcut, fp16 hi [C][KSC], k = ci
   const uint16_t* wsl;     //   (KSC = CIN rounded up to 32)
   const float* bs;         //   shortcut bias [C]
+  const uint8_t* img8;     // block 1 fused with the stem: the decoded image [N, H, W, 3] (uint8)
+  const float* imgf;       //   or float NHWC; x is then unused
+  const float* wst;        //   stem Conv2D(16, 1x1) weights [3][ldst] and bias [16]
+  const float* bst;
+  int ldst;
   float* y;                // non-pool: [N, H, W, C] = x + conv;  pool: [N, ceil(H/2), ceil(W/2), C]
   int n, h, w;             //   = MaxPool2D(2, 'same')(conv) + Conv2D(1x1, stride 2)(x)
   int tiles_h, tiles_w;    // set by resblk_launch

@@ -71,6 +71,23 @@ __device__ __forceinline__ void split2(f32x2 v, f16x2& h, f16x2& l) {
   l = __builtin_convertvector((v - hf) * LO_SCALE, f16x2);
 }
 
+// the 3 channels of image pixel `pix` (uint8 decoded PNG or float NHWC), as floats
+__device__ __forceinline__ float4 image_px(const ResBlkArgs& a, int64_t pix) {
+  if (a.img8) {
+    const uint8_t* p = a.img8 + pix * 3;
+    return make_float4((float)p[0], (float)p[1], (float)p[2], 0.f);
+  }
+  const float* p = a.imgf + pix * 3;
+  return make_float4(p[0], p[1], p[2], 0.f);
+}
+// Conv2D(16, 1x1) stem channel co of one pixel, in the stem kernel's order (nets.hip od_stem_kernel)
+__device__ __forceinline__ float stem_ch(const ResBlkArgs& a, float4 x, int co) {
+  float acc = x.x * a.wst[0 * a.ldst + co];
+  acc = fmaf(x.y, a.wst[1 * a.ldst + co], acc);
+  acc = fmaf(x.z, a.wst[2 * a.ldst + co], acc);
+  return acc + a.bst[co];
+}
+
 template <int CIN, int C, bool POOL>
 struct Geo {
   static constexpr int WN = 1;                     // waves along N: each wave owns all C columns,
@@ -113,7 +130,8 @@ struct Geo {
   static_assert(NT % QPP == 0, "a thread's channel quad is fixed");
 };
 
-template <int CIN, int C, bool POOL>
+// STEM: the block input is the stem Conv2D(16, 1x1) of the image, computed while staging (block 1)
+template <int CIN, int C, bool POOL, bool STEM>
 __global__ void __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(ResBlkArgs a) {
   using G = Geo<CIN, C, POOL>;
   constexpr int XC = G::XC, XPS = G::XPS, TPS = G::TPS, MT1 = G::MT1, MT2 = G::MT2, NTW = G::NTW;
@@ -140,7 +158,7 @@ __global__ void __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(R
   float4 pre[MAXT];
   uint32_t valid = 0;
   {
-    const float* xc = a.x + (int64_t)clip * a.h * a.w * CIN + 4 * q;
+    const float* xc = STEM ? nullptr : a.x + (int64_t)clip * a.h * a.w * CIN + 4 * q;
 #pragma unroll
     for (int j = 0; j < MAXT; ++j) {
       const int px = (tid + j * NT) / QPP;
@@ -152,7 +170,11 @@ __global__ void __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(R
 #if RB_EXP == 1
           pre[j] = make_float4(0.01f * ih, 0.02f * iw, 0.f, 1.f);
 #else
-          pre[j] = *reinterpret_cast<const float4*>(xc + (ih * a.w + iw) * CIN);
+          if constexpr (STEM) {
+            pre[j] = image_px(a, ((int64_t)clip * a.h + ih) * a.w + iw);
+          } else {
+            pre[j] = *reinterpret_cast<const float4*>(xc + (ih * a.w + iw) * CIN);
+          }
 #endif
           valid |= 1u << j;
         }
@@ -171,7 +193,7 @@ __global__ void __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(R
   if constexpr (POOL) {
     const int p = col;                            // this lane's A row (pooled pixel of the tile)
     const int pr = (p & 3) >> 1, pc = 2 * (p >> 2) + (p & 1);
-    const float* xc = a.x + (int64_t)clip * a.h * a.w * CIN;
+    const float* xc = STEM ? nullptr : a.x + (int64_t)clip * a.h * a.w * CIN;
 #pragma unroll
     for (int s = 0; s < KSC; ++s) {
       const int ci = 32 * s + 8 * grp;
@@ -186,9 +208,17 @@ __global__ void __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(R
         const int ih = h0 + 2 * (wm * (MT2 / 2) + 2 * j + pr), iw = w0 + 2 * pc;
         scx[s][j][0] = scx[s][j][1] = make_float4(0.f, 0.f, 0.f, 0.f);
         if (ci < CIN && ih < a.h && iw < a.w) {
-          const float* src = xc + (ih * a.w + iw) * CIN + ci;
-          scx[s][j][0] = *reinterpret_cast<const float4*>(src);
-          scx[s][j][1] = *reinterpret_cast<const float4*>(src + 4);
+          if constexpr (STEM) {
+            const float4 x = image_px(a, ((int64_t)clip * a.h + ih) * a.w + iw);
+            scx[s][j][0] = make_float4(stem_ch(a, x, ci), stem_ch(a, x, ci + 1), stem_ch(a, x, ci + 2),
+                                       stem_ch(a, x, ci + 3));
+            scx[s][j][1] = make_float4(stem_ch(a, x, ci + 4), stem_ch(a, x, ci + 5),
+                                       stem_ch(a, x, ci + 6), stem_ch(a, x, ci + 7));
+          } else {
+            const float* src = xc + (ih * a.w + iw) * CIN + ci;
+            scx[s][j][0] = *reinterpret_cast<const float4*>(src);
+            scx[s][j][1] = *reinterpret_cast<const float4*>(src + 4);
+          }
         }
       }
     }
@@ -206,6 +236,15 @@ __global__ void __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(R
 
   RB_MARK(1);
   // ---- stage: BN1 + ELU once per element, split hi/lo; zero outside the image (conv padding) ----
+  float stw[3][4], stb[4];   // STEM: this thread's stem weights (channels 4q .. 4q+3)
+  if constexpr (STEM) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) stw[k][c] = a.wst[k * a.ldst + 4 * q + c];
+      stb[c] = a.bst[4 * q + c];
+    }
+  }
   {
     const float4 sc4 = *reinterpret_cast<const float4*>(a.s1 + 4 * q);
     const float4 sh4 = *reinterpret_cast<const float4*>(a.t1 + 4 * q);
@@ -215,7 +254,19 @@ __global__ void __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(R
     for (int j = 0; j < MAXT; ++j) {
       const int px = (tid + j * NT) / QPP;
       if (px >= G::XNP) continue;
-      f32x2 v01 = {pre[j].x, pre[j].y}, v23 = {pre[j].z, pre[j].w};
+      float4 xv = pre[j];
+      if constexpr (STEM) {   // stem channels 4q .. 4q+3, in od_stem_kernel's order
+        float o[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          float acc = pre[j].x * stw[0][c];
+          acc = fmaf(pre[j].y, stw[1][c], acc);
+          acc = fmaf(pre[j].z, stw[2][c], acc);
+          o[c] = acc + stb[c];
+        }
+        xv = make_float4(o[0], o[1], o[2], o[3]);
+      }
+      f32x2 v01 = {xv.x, xv.y}, v23 = {xv.z, xv.w};
       const bool ok = (valid >> j) & 1u;
       const f32x2 u01 = elu2(v01 * sc01 + sh01), u23 = elu2(v23 * sc23 + sh23);
       v01 = ok ? u01 : f32x2{0.f, 0.f};
@@ -468,10 +519,10 @@ __global__ void __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(R
   RB_MARK(7);
 }
 
-template <int CIN, int C, bool POOL>
+template <int CIN, int C, bool POOL, bool STEM = false>
 hipError_t launch(const ResBlkArgs& a, hipStream_t s) {
   const int total = a.n * a.tiles_h * a.tiles_w;
-  hipLaunchKernelGGL((resblk_kernel<CIN, C, POOL>), dim3(total), dim3(NT), 0, s, a);
+  hipLaunchKernelGGL((resblk_kernel<CIN, C, POOL, STEM>), dim3(total), dim3(NT), 0, s, a);
   return hipGetLastError();
 }
 
@@ -495,7 +546,10 @@ hipError_t resblk_launch(ResBlkArgs a, int cin, int c, bool pool, hipStream_t s)
   a.tiles_h = (a.h + TH - 1) / TH;
   a.tiles_w = (a.w + TW - 1) / TW;
   if ((int64_t)a.n * a.tiles_h * a.tiles_w > 0x7fffffffLL) return hipErrorInvalidValue;
-  if (cin == 16) return launch<16, 32, true>(a, s);
+  if (cin == 16) {
+    if (a.img8 || a.imgf) return launch<16, 32, true, true>(a, s);
+    return launch<16, 32, true>(a, s);
+  }
   return launch<32, 32, false>(a, s);
 }
 
