@@ -33,6 +33,20 @@ F16X3_PEAK_TFS = F16_MFMA_PEAK_TFS / 3
 OD_FE_BYTES = 48000 + 128 * 151 * 4 + 151 * 4          # 125 916 B/clip
 
 
+def pmc_traffic(workload, stage, clips):
+    """HBM bytes per launch of `stage` from the committed PMC capture of this workload
+    (tools/gpu/pmc_traffic.sh -> profiles/pmc_traffic_<workload>.json), scaled to this run's clips
+    per launch; None when no capture exists."""
+    path = os.path.join(REPO, 'profiles', f'pmc_traffic_{workload}.json')
+    try:
+        d = json.load(open(path))
+        st = d['stages'][stage]
+        per_clip = st['traffic_bytes_per_launch'] / d['clips_per_launch'][stage]
+        return per_clip * min(clips, d['clips_per_launch'][stage]), os.path.relpath(path, REPO)
+    except (OSError, KeyError, ValueError, ZeroDivisionError):
+        return None, None
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -204,6 +218,7 @@ def main():
                 'arith': '3xFP16 on f16 MFMA (peak = f16 dense / 3)' if stage == 'conv' else 'f32 MFMA'}
     roof.update({'kernel': stage, 'launches': launches, 'avg_launch_ms': ms / max(launches, 1),
                  'work_per_launch': work / max(launches, 1)})
+    roof['traffic'], roof['traffic_source'] = pmc_traffic(wl, stage, clips)
     stages = {s: {'ms': round(v[0], 3), 'launches': v[1],
                   ('GB/s' if s in ('od_fe', 'si_fe') else 'TFLOP/s'):
                       round(v[2] / (v[0] * 1e-3) / (1e9 if s in ('od_fe', 'si_fe') else 1e12), 3)

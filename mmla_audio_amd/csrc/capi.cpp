@@ -833,11 +833,9 @@ int mmla_od_features(mmla_ctx* c, const int16_t* pcm, int64_t n, int64_t stride,
     CHK(out_ptr(c, norm, c0 * OD_PIX, cnt * OD_PIX, dev, S_OUT1, &a.norm));
     CHK(out_ptr(c, zcr, c0 * OD_W, cnt * OD_W, dev, S_OUT2, &a.zcr));
     CHK(out_ptr(c, img, c0 * OD_IMG, cnt * OD_IMG, dev, S_OUT3, &a.img));
-    if (!a.norm) {
-      void* ps = nullptr;
-      CHK(ws_get(c, S_FESCR, (size_t)cnt * OD_PIX * sizeof(float), &ps));
-      a.scratch = static_cast<float*>(ps);
-    }
+    void* ps = nullptr;
+    CHK(ws_get(c, S_FESCR, (size_t)cnt * OD_PIX * sizeof(float), &ps));
+    a.scratch = static_cast<float*>(ps);
     LAUNCH(c, MMLA_STAGE_OD_FE, od_fe_bytes(cnt, a), od_fe_launch(a, cnt, c->stream));
     CHK(copy_back(c, db, c0 * OD_PIX, a.db, cnt * OD_PIX, dev));
     CHK(copy_back(c, norm, c0 * OD_PIX, a.norm, cnt * OD_PIX, dev));

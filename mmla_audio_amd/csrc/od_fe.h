@@ -23,7 +23,7 @@ struct OdFeArgs {
   float* norm;              // [n,128,151] nullable
   float* zcr;               // [n,151]     nullable
   uint8_t* img;             // [n,128,151,3] nullable
-  float* scratch;           // [n,128,151] mel-power scratch; required when norm is null
+  float* scratch;           // [n,151,128] mel-power scratch (frame-major), required
 };
 
 void od_fe_build_tables(OdFeTables* t);

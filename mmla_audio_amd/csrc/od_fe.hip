@@ -102,9 +102,10 @@ __global__ void __launch_bounds__(NT) od_fe_kernel(OdFeArgs a) {
   int len = a.lens ? a.lens[clip] : a.clip_len;
   len = len < 0 ? 0 : (len > CLIP ? CLIP : len);
   const int16_t* src = a.pcm + clip * a.clip_stride;
-  // mel power of the whole clip goes to HBM-backed scratch (the norm output itself when requested:
-  // normalised in place), L2/MALL-resident until the normalisation pass below re-reads it
-  float* scr = (a.norm ? a.norm : a.scratch) + clip * (NMEL * NF);
+  // mel power of the whole clip goes to an HBM-backed scratch, frame-major [151][128] so every group
+  // stores whole 512-B frame rows; the normalisation pass re-reads it (L2/MALL-resident) in
+  // 8-band column blocks transposed through LDS
+  float* scr = a.scratch + clip * (NMEL * NF);
   // edge padding of the ZCR: samples before / after the clip repeat its first / last sample
   const int sg_first = (len > 0 ? src[0] : (int16_t)0) < 0;
   const int sg_last = (CLIP - 1 < len ? src[CLIP - 1] : (int16_t)0) < 0;
@@ -279,7 +280,7 @@ __global__ void __launch_bounds__(NT) od_fe_kernel(OdFeArgs a) {
         float acc = 0.0f;   // the band's non-zeros in order, then exact zero terms: same result
 #pragma unroll
         for (int j = 0; j < 10; ++j) acc = fmaf(mw[mh][j], p[j], acc);
-        scr[m * NF + f0 + f] = acc;
+        scr[(f0 + f) * NMEL + m] = acc;
         smax = fmaxf(smax, acc);
         smin = fminf(smin, acc);
       }
@@ -304,54 +305,64 @@ __global__ void __launch_bounds__(NT) od_fe_kernel(OdFeArgs a) {
   const float diff = d_max - d_min;
 
   float* db_out = a.db ? a.db + clip * (NMEL * NF) : nullptr;
-  const bool normed = db_out || a.norm;
-  if (normed) {
-    for (int e = lane; e < NMEL * NF; e += NT) {
-      float d = 10.0f * log10f(fmaxf(amin, scr[e])) - ref_db;
-      d = fmaxf(d, thr);
-      const float nv = (d - d_min) / diff;
-      if (db_out) db_out[e] = d;
-      scr[e] = nv;   // the norm output (or scratch the image reads)
-    }
-  }
+  float* nm_out = a.norm ? a.norm + clip * (NMEL * NF) : nullptr;
   if (a.zcr) {
     for (int f = lane; f < NF; f += NT) a.zcr[clip * NF + f] = (float)sm.zc[f] * (1.0f / 400.0f);
   }
-  if (a.img) {
-    if (normed) {
-      __threadfence();
-      __syncthreads();
-    }
-    // img[h][w][ch]: R = trunc(255 * zcr[w]) (float64), G = B = trunc(255 * (1 - norm[127-h][w]))
-    // (float64: numpy-1.21 '1 - np.float32' promotes); NaN -> 0.  One lane = 4 pixels = 3 words.
-    uint8_t* rb = reinterpret_cast<uint8_t*>(sm.pw);   // R byte per column (pw is free now)
-    for (int w = lane; w < NF; w += NT) {
-      const double v = ((double)sm.zc[w] / 400.0) * 255.0;
-      rb[w] = (uint8_t)(int)v;
-    }
+  // LDS of the group loop is free: [151][8] tiles of normalised / dB values + the R byte per column
+  constexpr int MB = 8;                                    // bands per column block
+  float* nvt = reinterpret_cast<float*>(&sm.t[0][0][0]);   // [NF][MB]
+  float* dbt = nvt + NF * MB;                               // [NF][MB]
+  uint8_t* rb = reinterpret_cast<uint8_t*>(sm.win);         // [NF]
+  static_assert(sizeof(sm.t) + sizeof(sm.pw) >= 2 * NF * MB * sizeof(float), "LDS tiles");
+  for (int w = lane; w < NF; w += NT) rb[w] = (uint8_t)(int)(((double)sm.zc[w] / 400.0) * 255.0);
+  for (int mb = 0; mb < NMEL / MB; ++mb) {
     __syncthreads();
-    uint32_t* out = reinterpret_cast<uint32_t*>(a.img + clip * (NMEL * NF * 3));
-    for (int qd = lane; qd < NMEL * NF / 4; qd += NT) {
-      uint32_t by[12];
+    for (int i = lane; i < NF * MB / 4; i += NT) {            // frame t, quad of bands
+      const int t = i / (MB / 4), qd = i - t * (MB / 4);
+      const float4 p4 = *reinterpret_cast<const float4*>(scr + t * NMEL + MB * mb + 4 * qd);
+      const float pv[4] = {p4.x, p4.y, p4.z, p4.w};
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int px = 4 * qd + j;
-        const int h = px / NF, w = px - h * NF;
-        float nv = scr[(NMEL - 1 - h) * NF + w];
-        if (!normed) {
-          float d = 10.0f * log10f(fmaxf(amin, nv)) - ref_db;
-          d = fmaxf(d, thr);
-          nv = (d - d_min) / diff;
-        }
-        const double v = (1.0 - (double)nv) * 255.0;
-        const uint32_t gb = (v >= 0.0) ? ((uint32_t)(int)v & 255u) : 0u;   // NaN fails v >= 0
-        by[3 * j] = rb[w];
-        by[3 * j + 1] = gb;
-        by[3 * j + 2] = gb;
+        float d = 10.0f * log10f(fmaxf(amin, pv[j])) - ref_db;
+        d = fmaxf(d, thr);
+        dbt[t * MB + 4 * qd + j] = d;
+        nvt[t * MB + 4 * qd + j] = (d - d_min) / diff;
       }
+    }
+    __syncthreads();
+    if (db_out || nm_out) {                                   // rows m = 8 mb .. 8 mb + 7
+      for (int e = lane; e < MB * NF; e += NT) {
+        const int r = e / NF, t = e - r * NF;
+        const int o = (MB * mb + r) * NF + t;
+        if (db_out) db_out[o] = dbt[t * MB + r];
+        if (nm_out) nm_out[o] = nvt[t * MB + r];
+      }
+    }
+    if (a.img) {
+      // image rows h = 127 - m: the block is 8 whole rows of 453 B, word aligned
+      // R = trunc(255 * zcr[w]) (float64), G = B = trunc(255 * (1 - norm)) (float64: numpy-1.21
+      // '1 - np.float32' promotes); NaN -> 0
+      const int h_lo = NMEL - MB * (mb + 1);
+      uint32_t* out = reinterpret_cast<uint32_t*>(a.img + clip * (NMEL * NF * 3) + h_lo * NF * 3);
+      for (int wd = lane; wd < MB * NF * 3 / 4; wd += NT) {
+        uint32_t word = 0;
 #pragma unroll
-      for (int k = 0; k < 3; ++k)
-        out[3 * qd + k] = by[4 * k] | (by[4 * k + 1] << 8) | (by[4 * k + 2] << 16) | (by[4 * k + 3] << 24);
+        for (int j = 0; j < 4; ++j) {
+          const int q = 4 * wd + j;
+          const int hr = q / (NF * 3), r = q - hr * (NF * 3);
+          const int w = r / 3, ch = r - w * 3;
+          uint32_t byte;
+          if (ch == 0) {
+            byte = rb[w];
+          } else {
+            const double v = (1.0 - (double)nvt[w * MB + (MB - 1 - hr)]) * 255.0;
+            byte = (v >= 0.0) ? ((uint32_t)(int)v & 255u) : 0u;   // NaN fails v >= 0
+          }
+          word |= byte << (8 * j);
+        }
+        out[wd] = word;
+      }
     }
   }
   }
@@ -363,7 +374,7 @@ size_t od_fe_smem_bytes() { return sizeof(Smem); }
 
 hipError_t od_fe_launch(const OdFeArgs& a, int64_t n_clips, hipStream_t stream) {
   if (n_clips <= 0) return hipSuccess;
-  if (!a.norm && !a.scratch) return hipErrorInvalidValue;
+  if (!a.scratch) return hipErrorInvalidValue;
   hipLaunchKernelGGL(od_fe_kernel, dim3((unsigned)n_clips), dim3(NT), 0, stream, a);
   return hipGetLastError();
 }

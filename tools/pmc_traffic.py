@@ -1,0 +1,59 @@
+"""Per-dispatch HBM bytes of the roofline kernels from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes
+(dev tool).  FETCH_SIZE is doubled (gfx950: MI355X_MICROARCH.md, HBM section); both counters are KiB.
+usage: python tools/pmc_traffic.py <workload> <fetch_dir> <write_dir>"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+STAGE = {  # kernel-name substring -> bench stage (mmla.h MMLA_STAGE_*)
+    'resblk_kernel': 'conv', 'conv_h3_kernel': 'conv', 'conv_kernel': 'conv',
+    'od_fe_kernel': 'od_fe', 'si_fe_kernel': 'si_fe', 'bilstm_kernel': 'lstm',
+}
+
+
+def read(d, ctr):
+    out = defaultdict(lambda: [0.0, set()])
+    for f in glob.glob(os.path.join(d, '**', '*counter_collection.csv'), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if r['Counter_Name'] != ctr:
+                continue
+            k = r['Kernel_Name']
+            out[k][0] += float(r['Counter_Value']) * 1024.0
+            out[k][1].add(r['Dispatch_Id'])
+    return out
+
+
+def main():
+    wl, fdir, wdir = sys.argv[1:4]
+    fe, wr = read(fdir, 'FETCH_SIZE'), read(wdir, 'WRITE_SIZE')
+    kernels = {}
+    stages = defaultdict(lambda: {'read_bytes': 0.0, 'write_bytes': 0.0, 'dispatches': 0})
+    for k in fe:
+        stage = next((v for s, v in STAGE.items() if s in k), None)
+        if stage is None:
+            continue
+        rd = 2.0 * fe[k][0]
+        w = wr[k][0] if k in wr else 0.0
+        n = len(fe[k][1])
+        kernels[k.replace('(anonymous namespace)::', '')[:100]] = {
+            'dispatches': n, 'read_bytes_per_dispatch': rd / n, 'write_bytes_per_dispatch': w / n}
+        stages[stage]['read_bytes'] += rd
+        stages[stage]['write_bytes'] += w
+        stages[stage]['dispatches'] += n
+    st = {s: {'dispatches': v['dispatches'],
+              'traffic_bytes_per_launch': (v['read_bytes'] + v['write_bytes']) / max(v['dispatches'], 1),
+              'read_bytes_per_launch': v['read_bytes'] / max(v['dispatches'], 1),
+              'write_bytes_per_launch': v['write_bytes'] / max(v['dispatches'], 1)}
+          for s, v in stages.items()}
+    # clips each launch processed: the library's OD micro-batch (4096) / the od_features bench batch
+    cpl = {s: 4096 for s in st}
+    json.dump({'workload': wl, 'clips_per_launch': cpl, 'note': 'rocprofv3 --pmc FETCH_SIZE (x2, gfx950) and WRITE_SIZE in '
+               'separate passes over `bench.py --workload %s --steps 1 --warmup 0`' % wl,
+               'stages': st, 'kernels': kernels}, sys.stdout, indent=1)
+
+
+if __name__ == '__main__':
+    main()
