@@ -280,7 +280,10 @@ def main():
         line = {
             'metric': METRIC, 'value': value, 'unit': 'clips/s', 'n_gpus': world,
             'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': dt / args.steps * 1e3,
-            'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32',
+            'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
+            # convolutions: error-compensated 3xFP16 on f16 MFMA with f32 accumulation; front-ends
+            # f32 (OD) / f64 (SI); LSTM, heads f32
+            'dtype': 'f16x3+f32' if wl == 'od_pipeline' else ('f64+f16x3' if wl == 'si_pipeline' else 'f32'),
             'data': f'synthetic: {clips} x {clip_len / 16000:g} s 16 kHz int16 clips per GPU generated '
                     f'in HBM (5 classes, SURVEY 8d); seeded synthetic weights in the reference '
                     f'variables.index layout (trained blobs absent)',
