@@ -15,7 +15,9 @@
  *   - A context is not thread-safe: use one per thread / per GPU.  The multi-GPU driver (one process
  *     per GPU, RCCL all-gather of logits) lives above this ABI.
  *   - PCM is 16 kHz mono int16; clip c starts at pcm + c * clip_stride (in samples) and has
- *     lens[c] valid samples (lens == NULL: every clip has clip_len samples).
+ *     lens[c] valid samples (lens == NULL: every clip has clip_len samples).  Without lens the
+ *     stride may be smaller than clip_len: overlapping windows of one signal (the offline
+ *     segmentation of overlap_detection_post_processing.py:23-85 with step < window).
  */
 #ifndef MMLA_H_
 #define MMLA_H_

@@ -260,6 +260,18 @@ class Context:
                                               _ptr(probs), _ptr(am), 0), 'mmla_od_pipeline')
         return probs, am
 
+    def od_pipeline_strided(self, signal, n, stride, clip_len):
+        """OD pipeline over n windows of one long int16 signal: window c = signal[c*stride :
+        c*stride + clip_len] (overlapping when stride < clip_len; no host-side copies)."""
+        sig = np.ascontiguousarray(signal, dtype=np.int16).reshape(-1)
+        if n < 0 or (n > 0 and (n - 1) * stride + clip_len > sig.size):
+            raise MmlaError(f'{n} windows of {clip_len} at stride {stride} exceed {sig.size} samples')
+        probs = np.empty((n, 2), np.float32)
+        am = np.empty(n, np.int32)
+        self._check(self.lib.mmla_od_pipeline(self.h, _ptr(sig), n, stride, None, clip_len,
+                                              _ptr(probs), _ptr(am), 0), 'mmla_od_pipeline')
+        return probs, am
+
     def si_pipeline(self, pcm, lens=None):
         a, ln, L = self._pcm(pcm, lens)
         n = a.shape[0]

@@ -330,6 +330,16 @@ int stage_pcm(mmla_ctx* c, const int16_t* pcm, int64_t c0, int64_t cnt, int64_t 
   int64_t width = lens ? std::min<int64_t>(need, stride) : std::min<int64_t>(need, clip_len);
   if (width < 1) width = 1;
   void* dp = nullptr;
+  if (!lens && stride < width) {
+    // overlapping windows of one signal (segmentation with step < window): copy the covered span
+    // once and let the kernels read window c at c * stride
+    const int64_t span = (cnt - 1) * stride + width;
+    CHK(ws_get(c, S_PCM, (size_t)span * sizeof(int16_t), &dp));
+    HIPCHK(c, hipMemcpyAsync(dp, pcm + c0 * stride, span * sizeof(int16_t), hipMemcpyHostToDevice,
+                             c->stream));
+    *out = {static_cast<int16_t*>(dp), stride, nullptr, (int32_t)std::min<int64_t>(clip_len, width)};
+    return MMLA_OK;
+  }
   CHK(ws_get(c, S_PCM, (size_t)cnt * width * sizeof(int16_t), &dp));
   HIPCHK(c, hipMemcpy2DAsync(dp, width * sizeof(int16_t), pcm + c0 * stride, stride * sizeof(int16_t),
                              width * sizeof(int16_t), cnt, hipMemcpyHostToDevice, c->stream));
@@ -659,7 +669,7 @@ bool bad_pcm_args(const int16_t* pcm, int64_t n, int64_t stride, const int32_t* 
                   int32_t clip_len) {
   if (n < 0 || (n > 0 && !pcm)) return true;
   if (!lens && clip_len < 0) return true;
-  if (!lens && n > 1 && stride < clip_len) return true;
+  if (!lens && n > 1 && stride < 1) return true;   // stride < clip_len: overlapping windows
   return false;
 }
 

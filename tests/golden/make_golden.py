@@ -25,8 +25,12 @@ numpy note: this image has numpy 2.2 (NEP 50 promotion).  Under the reference's 
 therefore differs from the numpy-1.21 result in at most a few pixels by 1 LSB where 1-x sits on a
 quantisation edge (tests allow that, see tests/test_oracle_golden.py).
 
-Output: tests/golden/od_golden.npz, si_golden.npz (small, compressed).
+  * the offline OD segmentation (overlap_detection_post_processing.py:23-85): segment count, names
+    and the bytes of every segment WAV it writes, mono and stereo (seg_golden.npz).
+
+Output: tests/golden/od_golden.npz, si_golden.npz, seg_golden.npz (small, compressed).
 """
+import hashlib
 import io
 import os
 import sys
@@ -153,6 +157,57 @@ SI_CASES = [
 ]
 
 
+SEG_CASES = [
+    # (name, channels, samples per channel, win_time, step_time)
+    ('mono_5p3s_1p5_1p5', 1, 84800, 1.5, 1.5),    # 3 segments, 12 800-sample tail dropped
+    ('mono_4s_1p5_0p5', 1, 64000, 1.5, 0.5),      # overlapping windows
+    ('mono_exact_3s', 1, 48000, 1.5, 1.5),        # exact multiple
+    ('stereo_3p2s_1p5_1p5', 2, 51200, 1.5, 1.5),  # interleaved frames
+]
+
+
+def _segmentation_cases(ofg_mod, tmp):
+    """Run the reference's segmentation() on synthetic WAVs; record every segment file it writes."""
+    import wave
+    sys.modules['overlap_features_generator'] = ofg_mod
+    _module('overlap_degree_distribution')
+    _module('noisereduce')
+    _module('soundfile')
+    post = _load_reference('OverlapDetection/scripts/overlap_detection_post_processing.py', 'ref_post')
+    seg = {'names': np.array([c[0] for c in SEG_CASES])}
+    for i, (name, ch, n, win, step) in enumerate(SEG_CASES):
+        src = os.path.join(tmp, f'segsrc{i}')
+        dst = os.path.join(tmp, f'segdst{i}')
+        os.makedirs(src)
+        os.makedirs(dst)
+        pcm = np.stack([synth.clip(30 + i * 2 + c, n) for c in range(ch)], axis=1)   # [n, ch]
+        fname = f'conv{i}.wav'
+        for path in (os.path.join(src, fname), src + '\\' + fname):
+            # the reference joins with a Windows separator (:33): on Linux that names a sibling file
+            with wave.open(path, 'wb') as w:
+                w.setnchannels(ch)
+                w.setsampwidth(2)
+                w.setframerate(16000)
+                w.writeframes(pcm.astype('<i2').tobytes())
+        post.segmentation(src, dst, win, step)
+        # on Linux the reference's base name keeps the 'segsrc<i>\\' prefix: take its one directory
+        (sub,) = os.listdir(dst)
+        out = sorted(os.listdir(os.path.join(dst, sub)), key=lambda f: int(f.split('_')[-3]))
+        # inputs are regenerated by the tests from oracle.synth (seeds 30 + 2 i + channel)
+        seg[f'params_{i}'] = np.array([ch, n, win, step])
+        seg[f'files_{i}'] = np.array([f.split('\\')[-1] for f in out])
+        digests = []
+        for j, f in enumerate(out):
+            with open(os.path.join(dst, sub, f), 'rb') as fh:
+                b = fh.read()
+            seg[f'head_{i}_{j}'] = np.frombuffer(b[:44], np.uint8)     # RIFF/fmt/data header
+            seg[f'len_{i}_{j}'] = np.array(len(b))
+            digests.append(hashlib.sha256(b).hexdigest())
+        seg[f'sha256_{i}'] = np.array(digests)
+        print('SEG', name, len(out), 'segments')
+    return seg
+
+
 def main():
     _install_stubs()
     ofg_mod = _load_reference('OverlapDetection/scripts/overlap_features_generator.py', 'ref_ofg')
@@ -196,6 +251,8 @@ def main():
     si['delta_out'] = si_mod.delta(dx, 2)
     si['delta2_out'] = si_mod.delta(si_mod.delta(dx, 2), 2)
 
+    seg = _segmentation_cases(ofg_mod, tmp)
+    np.savez_compressed(os.path.join(HERE, 'seg_golden.npz'), **seg)
     np.savez_compressed(os.path.join(HERE, 'od_golden.npz'), **od)
     np.savez_compressed(os.path.join(HERE, 'si_golden.npz'), **si)
     print('wrote', os.path.join(HERE, 'od_golden.npz'), os.path.join(HERE, 'si_golden.npz'))
