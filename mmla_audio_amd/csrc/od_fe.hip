@@ -280,7 +280,8 @@ __global__ void __launch_bounds__(NT) od_fe_kernel(OdFeArgs a) {
         float acc = 0.0f;   // the band's non-zeros in order, then exact zero terms: same result
 #pragma unroll
         for (int j = 0; j < 10; ++j) acc = fmaf(mw[mh][j], p[j], acc);
-        scr[(f0 + f) * NMEL + m] = acc;
+        // power_to_db's first term, 10 log10(max(amin, S)), rounded exactly as in the epilogue
+        scr[(f0 + f) * NMEL + m] = 10.0f * log10f(fmaxf(1e-10f, acc));
         smax = fmaxf(smax, acc);
         smin = fminf(smin, acc);
       }
@@ -316,18 +317,39 @@ __global__ void __launch_bounds__(NT) od_fe_kernel(OdFeArgs a) {
   uint8_t* rb = reinterpret_cast<uint8_t*>(sm.win);         // [NF]
   static_assert(sizeof(sm.t) + sizeof(sm.pw) >= 2 * NF * MB * sizeof(float), "LDS tiles");
   for (int w = lane; w < NF; w += NT) rb[w] = (uint8_t)(int)(((double)sm.zc[w] / 400.0) * 255.0);
-  for (int mb = 0; mb < NMEL / MB; ++mb) {
-    __syncthreads();
-    for (int i = lane; i < NF * MB / 4; i += NT) {            // frame t, quad of bands
+  const float inv_diff = 1.0f / diff;
+  // the block's scratch reads are issued one block ahead (registers) so their latency hides
+  constexpr int RPL = (NF * MB / 4 + NT - 1) / NT;          // float4 per lane per block (5)
+  float4 cur[RPL], nxt[RPL];
+  auto fetch = [&](int mb_, float4 (&dst)[RPL]) {
+#pragma unroll
+    for (int r = 0; r < RPL; ++r) {
+      const int i = lane + NT * r;
       const int t = i / (MB / 4), qd = i - t * (MB / 4);
-      const float4 p4 = *reinterpret_cast<const float4*>(scr + t * NMEL + MB * mb + 4 * qd);
-      const float pv[4] = {p4.x, p4.y, p4.z, p4.w};
+      if (i < NF * MB / 4) dst[r] = *reinterpret_cast<const float4*>(scr + t * NMEL + MB * mb_ + 4 * qd);
+    }
+  };
+  fetch(0, nxt);
+  for (int mb = 0; mb < NMEL / MB; ++mb) {
+#pragma unroll
+    for (int r = 0; r < RPL; ++r) cur[r] = nxt[r];
+    if (mb + 1 < NMEL / MB) fetch(mb + 1, nxt);
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < RPL; ++r) {                           // frame t, quad of bands
+      const int i = lane + NT * r;
+      if (i >= NF * MB / 4) break;
+      const int t = i / (MB / 4), qd = i - t * (MB / 4);
+      const float pv[4] = {cur[r].x, cur[r].y, cur[r].z, cur[r].w};
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        float d = 10.0f * log10f(fmaxf(amin, pv[j])) - ref_db;
+        float d = pv[j] - ref_db;   // pv = 10 log10(max(amin, S)) from the mel pass
         d = fmaxf(d, thr);
         dbt[t * MB + 4 * qd + j] = d;
-        nvt[t * MB + 4 * qd + j] = (d - d_min) / diff;
+        // normalize_matrix's (x - min) / (max - min) as a multiply by the reciprocal: <= 2 ulp from
+        // the division (image quantisation flips <= 1 LSB on ~1e-5 of pixels); 0 * inf = NaN
+        // keeps the digital-silence NaN
+        nvt[t * MB + 4 * qd + j] = (d - d_min) * inv_diff;
       }
     }
     __syncthreads();
@@ -345,23 +367,22 @@ __global__ void __launch_bounds__(NT) od_fe_kernel(OdFeArgs a) {
       // '1 - np.float32' promotes); NaN -> 0
       const int h_lo = NMEL - MB * (mb + 1);
       uint32_t* out = reinterpret_cast<uint32_t*>(a.img + clip * (NMEL * NF * 3) + h_lo * NF * 3);
-      for (int wd = lane; wd < MB * NF * 3 / 4; wd += NT) {
-        uint32_t word = 0;
+      // one lane = 4 consecutive pixels of the block (row-major) = 12 bytes = 3 words
+      for (int qd = lane; qd < MB * NF / 4; qd += NT) {
+        uint32_t by[12];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const int q = 4 * wd + j;
-          const int hr = q / (NF * 3), r = q - hr * (NF * 3);
-          const int w = r / 3, ch = r - w * 3;
-          uint32_t byte;
-          if (ch == 0) {
-            byte = rb[w];
-          } else {
-            const double v = (1.0 - (double)nvt[w * MB + (MB - 1 - hr)]) * 255.0;
-            byte = (v >= 0.0) ? ((uint32_t)(int)v & 255u) : 0u;   // NaN fails v >= 0
-          }
-          word |= byte << (8 * j);
+          const int p = 4 * qd + j;
+          const int hr = p / NF, w = p - hr * NF;
+          const double v = (1.0 - (double)nvt[w * MB + (MB - 1 - hr)]) * 255.0;
+          const uint32_t gb = (v >= 0.0) ? ((uint32_t)(int)v & 255u) : 0u;   // NaN fails v >= 0
+          by[3 * j] = rb[w];
+          by[3 * j + 1] = gb;
+          by[3 * j + 2] = gb;
         }
-        out[wd] = word;
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+          out[3 * qd + k] = by[4 * k] | (by[4 * k + 1] << 8) | (by[4 * k + 2] << 16) | (by[4 * k + 3] << 24);
       }
     }
   }
