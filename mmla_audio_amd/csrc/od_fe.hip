@@ -27,6 +27,12 @@
 #include "common.h"
 #include "od_fe.h"
 
+#ifndef FE_EXP
+#define FE_EXP 0   // 1: per-phase s_memtime totals of the first 4096 clips (tools/fe_timeline.py)
+#endif
+#if FE_EXP
+__device__ unsigned long long g_fe_t[4096 * 8];
+#endif
 namespace {
 
 constexpr int N_FFT = 400;
@@ -145,6 +151,18 @@ __global__ void __launch_bounds__(NT) od_fe_kernel(OdFeArgs a) {
     for (int j = 0; j < 10; ++j) mw[mh][j] = tb.mel_w[m][j];
   }
 
+#if FE_EXP
+  unsigned long long tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long tlast = __builtin_amdgcn_s_memtime();
+#define FE_MARK(k)                                                   \
+  do {                                                               \
+    const unsigned long long tn = __builtin_amdgcn_s_memtime();      \
+    tacc[k] += tn - tlast;                                           \
+    tlast = tn;                                                      \
+  } while (0)
+#else
+#define FE_MARK(k)
+#endif
   float smax = 0.0f, smin = INFINITY;
   for (int g = 0; g < NG; ++g) {
     const int f0 = g * F;
@@ -167,6 +185,7 @@ __global__ void __launch_bounds__(NT) od_fe_kernel(OdFeArgs a) {
     }
     if (g + 1 < NG && fast(g + 1)) prefetch(g + 1);
     __syncthreads();
+    FE_MARK(0);
     // ---- zero crossings of the group's frames (edge padding; transitions at padded positions
     //      160 f + 1 .. 160 f + 399, signbit semantics) ---------------------------------------------
     // lane l < 52 counts the transitions (w - 1, w) at window positions w = 20 l .. 20 l + 19; frame f
@@ -205,6 +224,7 @@ __global__ void __launch_bounds__(NT) od_fe_kernel(OdFeArgs a) {
       }
       __syncthreads();
     }
+    FE_MARK(1);
     // ---- pass 1: real 16-point DFT over n1 of x[25 n1 + n2] * hann, times W400^(n2 k1) ----------
 #pragma unroll
     for (int r = 0; r < (F * 25 + NT - 1) / NT; ++r) {
@@ -233,6 +253,7 @@ __global__ void __launch_bounds__(NT) od_fe_kernel(OdFeArgs a) {
       }
     }
     __syncthreads();
+    FE_MARK(2);
     // ---- pass 2a: DFT-5 over a of t[k1][5a + b], times W25^(b c), in place at t[k1][5c + b] -------
 #pragma unroll
     for (int rr = 0; rr < (F * 45 + NT - 1) / NT; ++rr) {
@@ -249,6 +270,7 @@ __global__ void __launch_bounds__(NT) od_fe_kernel(OdFeArgs a) {
       }
     }
     __syncthreads();
+    FE_MARK(3);
     // ---- pass 2b: DFT-5 over b -> X[k1 + 16 (c + 5 d)] -> power; bins > 200 fold onto 400 - k ---
 #pragma unroll
     for (int rr = 0; rr < (F * 45 + NT - 1) / NT; ++rr) {
@@ -269,6 +291,7 @@ __global__ void __launch_bounds__(NT) od_fe_kernel(OdFeArgs a) {
       }
     }
     __syncthreads();
+    FE_MARK(4);
     // ---- mel: S[m][f] = sum_j w[m][j] * P[f][start_m + j] -> scratch ---------------------------------
 #pragma unroll
     for (int mh = 0; mh < NMEL / NT; ++mh) {
@@ -287,6 +310,7 @@ __global__ void __launch_bounds__(NT) od_fe_kernel(OdFeArgs a) {
       }
     }
   }
+  FE_MARK(5);
   // ---- clip max / min of the mel power (one wave: shuffles only) ----------------------------------
   smax = wave_max(smax);
   smin = wave_min(smin);
@@ -387,9 +411,20 @@ __global__ void __launch_bounds__(NT) od_fe_kernel(OdFeArgs a) {
     }
   }
   }
+#if FE_EXP
+  FE_MARK(6);
+  if (lane == 0 && clip < 4096)
+    for (int i = 0; i < 8; ++i) g_fe_t[clip * 8 + i] = tacc[i];
+#endif
 }
 
 }  // namespace
+
+#if FE_EXP
+extern "C" int mmla_debug_fe_times(unsigned long long* host) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_fe_t), sizeof(g_fe_t));
+}
+#endif
 
 size_t od_fe_smem_bytes() { return sizeof(Smem); }
 
