@@ -76,6 +76,9 @@ struct ProfRec {
 
 }  // namespace
 
+constexpr int64_t kOdMicrobatch = 4096;    // OD clips per internal micro-batch (30 GB of activations)
+constexpr int64_t kSiMicrobatch = 16384;
+
 struct mmla_ctx {
   bool prof_on = false;
   std::vector<ProfRec> prof_pending;
@@ -95,7 +98,7 @@ struct mmla_ctx {
   std::vector<void*> od_allocs, si_allocs;
   std::vector<void*> ws;
   std::vector<size_t> ws_size;
-  int64_t od_mb = 4096, si_mb = 16384;
+  int64_t od_mb = kOdMicrobatch, si_mb = kSiMicrobatch;
   int precision = MMLA_PREC_F16X3;
 };
 
@@ -749,8 +752,8 @@ int mmla_set_precision(mmla_ctx* c, int mode) {
 
 int mmla_set_microbatch(mmla_ctx* c, int64_t od, int64_t si) {
   if (!c || od < 0 || si < 0) return MMLA_E_INVALID;
-  if (od) c->od_mb = od;
-  if (si) c->si_mb = si;
+  c->od_mb = od ? od : kOdMicrobatch;   // 0 = the default (mmla.h)
+  c->si_mb = si ? si : kSiMicrobatch;
   return MMLA_OK;
 }
 

@@ -1,0 +1,65 @@
+"""Batch composition must not change any clip's result (the reference runs batch 1 per clip).
+
+Every kernel works per clip (the fused conv tiles never straddle clips), so a clip's outputs are
+bit-identical whether it runs alone, inside a large batch, or across micro-batch boundaries.
+"""
+import numpy as np
+import pytest
+
+from oracle import synth
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope='module')
+def ctx():
+    from mmla_audio_amd import _lib, weights
+    c = _lib.Context(0)
+    W = weights.synthetic(weights.OD, seed=21)
+    c.load_weights(weights.OD, weights.pack(weights.OD, W), 2)
+    Ws = weights.synthetic(weights.SI, seed=22, n_classes=8)
+    c.load_weights(weights.SI, weights.pack(weights.SI, Ws, 8), 8, 1)
+    return c
+
+
+def test_od_batch_invariance(ctx):
+    pcm = synth.batch(800, 37, 40000)
+    p_all, a_all = ctx.od_pipeline(pcm)
+    for i in (0, 17, 36):
+        p1, a1 = ctx.od_pipeline(pcm[i:i + 1])
+        assert np.array_equal(p1[0], p_all[i]) and a1[0] == a_all[i]
+
+
+def test_od_microbatch_boundaries(ctx):
+    pcm = synth.batch(900, 150, 40000)
+    p_ref, a_ref = ctx.od_pipeline(pcm)
+    ctx.set_microbatch(64, 0)            # 150 clips -> 64 + 64 + 22
+    try:
+        p, a = ctx.od_pipeline(pcm)
+        f = ctx.od_features(pcm[:70], db=False, zcr=False)
+        x = ctx.od_forward(f['img'])
+    finally:
+        ctx.set_microbatch(0, 0)   # back to the defaults
+    assert np.array_equal(p, p_ref) and np.array_equal(a, a_ref)
+    assert np.array_equal(x, p_ref[:70])
+
+
+def test_si_microbatch_boundaries(ctx):
+    lens = [24000 if i % 7 else 3000 for i in range(50)]
+    pcm = [synth.clip(1000 + i, n) for i, n in enumerate(lens)]
+    p_ref, a_ref, s_ref = ctx.si_pipeline(pcm)
+    ctx.set_microbatch(0, 16)            # 50 clips -> 16 + 16 + 16 + 2
+    try:
+        p, a, s = ctx.si_pipeline(pcm)
+    finally:
+        ctx.set_microbatch(0, 0)   # back to the defaults
+    assert np.array_equal(p, p_ref) and np.array_equal(a, a_ref) and np.array_equal(s, s_ref)
+
+
+def test_empty_batches(ctx):
+    p, a = ctx.od_pipeline(np.zeros((0, 40000), np.int16))
+    assert p.shape == (0, 2) and a.shape == (0,)
+    f = ctx.od_features(np.zeros((0, 40000), np.int16))
+    assert f['norm'].shape == (0, 128, 151)
+    x = ctx.od_forward(np.zeros((0, 128, 151, 3), np.float32))
+    assert x.shape == (0, 2)
