@@ -700,6 +700,10 @@ int mmla_create(int device, mmla_ctx** out) {
   c->stream = c->own_stream;
   OdFeTables ot;
   od_fe_build_tables(&ot);
+  if (!od_fe_tables_ok(ot)) {   // mel tap counts exceed the front-end kernel's unrolled taps
+    mmla_destroy(c);
+    return MMLA_E_INVALID;
+  }
   SiFeTables st;
   si_fe_build_tables(&st);
   if (hipMalloc(&c->od_tables, sizeof(OdFeTables)) != hipSuccess ||

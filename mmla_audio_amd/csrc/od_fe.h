@@ -11,6 +11,11 @@ struct OdFeTables {
   int mel_start[128];       // first non-zero bin of each Slaney mel band
   int mel_cnt[128];         // number of non-zero bins (<= 9)
   float mel_w[128][10];     // float32 band weights
+  // v2 (200-point complex FFT of the even/odd-packed frame, 20 x 10 Cooley-Tukey)
+  float hann2[200][2];      // (hann[2m], hann[2m + 1]) / 32768
+  float tw[20][10][2];      // W200^(k1 * n2)
+  float w400k[101][2];      // W400^k, k = 0..100 (even/odd split)
+  int mel_taps_lo, mel_taps_hi;   // max non-zeros over bands 0..63 / 64..127
 };
 
 struct OdFeArgs {
@@ -27,5 +32,6 @@ struct OdFeArgs {
 };
 
 void od_fe_build_tables(OdFeTables* t);
+bool od_fe_tables_ok(const OdFeTables& t);   // the mel tap counts fit the kernel's unrolling
 size_t od_fe_smem_bytes();
 hipError_t od_fe_launch(const OdFeArgs& a, int64_t n_clips, hipStream_t stream);

@@ -8,30 +8,56 @@
 //   zero_crossing_rate(400, 160)        :100  (edge padding, signbit crossings)
 //   generate_zcr_image + imsave + decode_png   :133-151, record_on_pc.py:156-158
 //
-// Layout / schedule: one workgroup = one wave = one clip (no block barriers beyond the wave's own),
-// ~16 KB of LDS, so ~10 clips are in flight per CU.  Frames go in groups of F = 5 (125 / 225 / 225 /
-// 640 lane tasks per pass, 88-100 % of the lanes busy): the group's reflect-padded 1040-sample
-// window is staged in LDS, the three DFT passes run in one LDS buffer, and the mel power goes to an
-// HBM-backed scratch (the norm output itself when it is requested).  The clip's normalisation needs
-// the clip-global max/min, so the scratch is re-read (L2/MALL-resident) once the last group is done.
-// 400-point real DFT per frame, factored n = 25*n1 + n2, k = k1 + 16*k2:
-//   pass 1 (25 tasks/frame): real 16-point DFT over n1 (via a complex 8-point FFT), k1 = 0..8,
-//                            times W400^(n2*k1)
-//   pass 2 (45 tasks/frame): 5-point DFTs over a (n2 = 5a + b), times W25^(b*c)
-//   pass 3 (45 tasks/frame): 5-point DFTs over b -> X[k1 + 16*(c + 5d)] -> |X|^2; bins > 200
-//                            fold onto 400 - k (conjugate symmetry) for k1 = 1..7
-//   mel: sparse Slaney filterbank (394 non-zeros, <= 9 per band) from the per-frame power.
+// Two kernels share the ABI (OdFeArgs); `od_fe_launch` runs v2 unless MMLA_FE_IMPL=1.
+//
+// v2 (default).  One wave = one clip (64-thread workgroups), frames in rounds of R = 6.  The
+// 400-point real DFT of a frame is ONE 200-point complex FFT of the even/odd-packed frame
+// z[m] = x[2m] + i x[2m+1] followed by the standard split
+//     X[k] = (Z[k] + conj Z[200-k]) / 2 - i W400^k (Z[k] - conj Z[200-k]) / 2,
+// and the 200-point FFT is Cooley-Tukey 20 x 10 with both sub-transforms as prime-factor (Good-
+// Thomas) FFTs (20 = 4 x 5, 10 = 2 x 5: no twiddles inside them):
+//   pass A  (60 lanes = 6 frames x n2 0..9):  DFT-20 over n1 of z[10 n1 + n2], x W200^(n2 k1)
+//   pass B  (2 x 60 lanes = 6 frames x k1):   DFT-10 over n2 -> Z[k1 + 20 k2]
+//   split   (per frame, k = lane, lane + 64): |X[k]|^2 and |X[200 - k]|^2 from Z[k], Z[200 - k]
+//   mel     (lane = bands m, m + 64):         sparse Slaney taps from registers, 10 log10 S
+// Only LDS dependencies inside ONE wave cross lanes in the round loop, and a wave's LDS operations
+// execute in issue order, so the loop has no s_barrier / s_waitcnt vmcnt(0): the next round's
+// window (register prefetch) and the mel-dB scratch stores stay in flight across passes.  The
+// clip's normalisation needs the clip-global max/min, so the dB rows go to a frame-major HBM
+// scratch that the epilogue re-reads (8-band column blocks, transposed through LDS).
+//
+// v1.  The earlier schedule (16 x 25 factoring of the real DFT, 5-frame groups, block barriers);
+// kept for A/B measurements.
+//
 // Arithmetic is float32 (the reference runs the FFT in float64 and stores complex64; the measured
-// deviation on the normalised log-mel is ~1e-6, tolerance 1e-4).  The scalar steps
+// deviation on the normalised log-mel is ~1e-5, tolerance 1e-4).  The scalar steps
 // that the reference does in float64 (ref dB, image quantisation) are done in float64 here.
 #include "common.h"
 #include "od_fe.h"
+
+#include <cstdlib>
 
 #ifndef FE_EXP
 #define FE_EXP 0   // 1: per-phase s_memtime totals of the first 4096 clips (tools/fe_timeline.py)
 #endif
 #if FE_EXP
 __device__ unsigned long long g_fe_t[4096 * 8];
+#define FE_T_INIT                                              \
+  unsigned long long tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};       \
+  unsigned long long tlast = __builtin_amdgcn_s_memtime();
+#define FE_MARK(k)                                                   \
+  do {                                                               \
+    const unsigned long long tn = __builtin_amdgcn_s_memtime();      \
+    tacc[k] += tn - tlast;                                           \
+    tlast = tn;                                                      \
+  } while (0)
+#define FE_T_STORE                                                   \
+  if (lane == 0 && clip < 4096)                                      \
+    for (int i_ = 0; i_ < 8; ++i_) g_fe_t[clip * 8 + i_] = tacc[i_];
+#else
+#define FE_T_INIT
+#define FE_MARK(k)
+#define FE_T_STORE
 #endif
 namespace {
 
@@ -40,20 +66,7 @@ constexpr int HOP = 160;
 constexpr int CLIP = 24000;
 constexpr int NF = 151;
 constexpr int NMEL = 128;
-constexpr int F = 5;             // frames per group: 25 F, 45 F, 128 F lane tasks per pass
-constexpr int NG = (NF + F - 1) / F;
-constexpr int WIN = (F - 1) * HOP + N_FFT;   // samples behind one group of frames
-constexpr int NT = 64;           // one wave per workgroup (= per clip): no block barriers
-
-struct Smem {                    // 15.9 KB: ~10 clips in flight per CU
-  int16_t win[WIN + 16];         // reflect-padded window of the group, base = 160 f0 - 200
-  cf t[F][9][25];                // pass 1 output, transformed in place by pass 2a
-  float pw[F][216];              // power spectrum (bins 0..200; 201.. stay 0 for the 10-tap mel dot)
-  int zc[NF + 1];                // ZCR counts of the clip
-  float hann[N_FFT];             // tables the lanes index per task (LDS, not L2 latency)
-  float w400[9][25][2];
-  float w25[5][5][2];
-};
+constexpr int NT = 64;           // one wave per workgroup (= per clip)
 
 MMLA_DEV void fft4(cf& a0, cf& a1, cf& a2, cf& a3) {
   cf s02 = cadd(a0, a2), d02 = csub(a0, a2), s13 = cadd(a1, a3), d13 = csub(a1, a3);
@@ -99,6 +112,414 @@ MMLA_DEV void dft5(cf x0, cf x1, cf x2, cf x3, cf x4, cf y[5]) {
   y[3] = csub(p2, cmul_negi(q2));
 }
 
+// DFT-20 in place, natural order in and out: prime-factor 4 x 5, input n = (5a + 4b) mod 20,
+// output k = (5c + 16d) mod 20 (W20^(nk) = W4^(ac) W5^(bd): no twiddles)
+MMLA_DEV void dft20(cf u[20]) {
+  cf t[5][4];
+#pragma unroll
+  for (int b = 0; b < 5; ++b) {
+    cf a0 = u[(4 * b) % 20], a1 = u[(5 + 4 * b) % 20], a2 = u[(10 + 4 * b) % 20],
+       a3 = u[(15 + 4 * b) % 20];
+    fft4(a0, a1, a2, a3);
+    t[b][0] = a0;
+    t[b][1] = a1;
+    t[b][2] = a2;
+    t[b][3] = a3;
+  }
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    cf y[5];
+    dft5(t[0][c], t[1][c], t[2][c], t[3][c], t[4][c], y);
+#pragma unroll
+    for (int d = 0; d < 5; ++d) u[(5 * c + 16 * d) % 20] = y[d];
+  }
+}
+
+// DFT-10 in place: prime-factor 2 x 5, input n = (5a + 2b) mod 10, output k = (5c + 6d) mod 10
+MMLA_DEV void dft10(cf v[10]) {
+  cf t[5][2];
+#pragma unroll
+  for (int b = 0; b < 5; ++b) {
+    const cf a0 = v[(2 * b) % 10], a1 = v[(5 + 2 * b) % 10];
+    t[b][0] = cadd(a0, a1);
+    t[b][1] = csub(a0, a1);
+  }
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    cf y[5];
+    dft5(t[0][c], t[1][c], t[2][c], t[3][c], t[4][c], y);
+#pragma unroll
+    for (int d = 0; d < 5; ++d) v[(5 * c + 6 * d) % 10] = y[d];
+  }
+}
+
+// power_to_db's per-element term 10 log10(max(amin, S)): v_log_f32 (log2) times 10 log10(2).  Every
+// use in the v2 kernel (elements, clip max, clip min) goes through this one function, so the clip
+// maximum maps to exactly d_max and the normalised maximum to exactly 1, as in the reference.
+MMLA_DEV float db10(float s) { return __log2f(fmaxf(1e-10f, s)) * 3.0102999566398120f; }
+
+// wave-local LDS ordering: a wave's DS operations execute in issue order, so lanes of ONE wave
+// only need the compiler not to move LDS accesses across this point (no s_barrier, no vmcnt wait)
+MMLA_DEV void lds_order() { asm volatile("" ::: "memory"); }
+
+// ================================================================================================
+namespace v2 {
+
+constexpr int R = 6;                              // frames per round
+constexpr int NR = (NF + R - 1) / R;              // 26 rounds
+constexpr int WIN = (R - 1) * HOP + N_FFT;        // 1200 samples behind one round
+constexpr int T_LO = 3, T_HI = 10;                // mel taps of bands 0..63 / 64..127 (host-checked)
+
+struct Smem {                      // 16.8 KB
+  int16_t win[WIN];                // reflect-padded window of the round, base = 160 f0 - 200
+  cf st[R][200];                   // per frame: pass A out [k1][n2] -> Z[k] -> power P[k] (floats)
+  int zc[NF + 1];                  // ZCR counts of the clip
+  uint8_t rb[NF + 1];              // image R byte per column
+  cf hann2[200];
+  cf tw[20][10];
+  cf w400[101];
+};
+static_assert(sizeof(int16_t) * WIN % 16 == 0, "st must stay 16-B aligned");
+
+// |X[k]|^2 and |X[200 - k]|^2 of the 400-point real DFT from Z[k], Z[200 - k] of the packed FFT
+MMLA_DEV void split_power(cf z, cf zr, cf w, float& pk, float& pnk) {
+  const cf h = {0.5f * (z.x + zr.x), 0.5f * (z.y - zr.y)};   // (Z[k] + conj Z[-k]) / 2 = E[k]
+  const cf b = {0.5f * (z.x - zr.x), 0.5f * (z.y + zr.y)};   // (Z[k] - conj Z[-k]) / 2 = i O[k]
+  const cf wb = cmul(w, b);
+  const cf c = {-wb.y, wb.x};                                 // i W^k B / 2
+  const cf x0 = csub(h, c);                                   // X[k]
+  const cf x1 = cadd(h, c);                                   // conj X[200 - k]
+  pk = fmaf(x0.x, x0.x, x0.y * x0.y);
+  pnk = fmaf(x1.x, x1.x, x1.y * x1.y);
+}
+
+__global__ void __launch_bounds__(NT, 3) od_fe_kernel(OdFeArgs a) {
+  __shared__ __attribute__((aligned(16))) Smem sm;
+  const OdFeTables& tb = *a.tables;
+  const int lane = threadIdx.x;
+  const int64_t clip = blockIdx.x;
+
+  int len = a.lens ? a.lens[clip] : a.clip_len;
+  len = len < 0 ? 0 : (len > CLIP ? CLIP : len);
+  const int16_t* src = a.pcm + clip * a.clip_stride;
+  float* scr = a.scratch + clip * (NMEL * NF);
+  // edge padding of the ZCR: samples before / after the clip repeat its first / last sample
+  const int sg_first = (len > 0 ? src[0] : (int16_t)0) < 0;
+  const int sg_last = (CLIP - 1 < len ? src[CLIP - 1] : (int16_t)0) < 0;
+
+  // the window of round r + 1 is loaded into registers (16-B chunks) while round r computes; rounds
+  // whose window leaves [0, len) take the scalar reflect / zero-fill path instead
+  constexpr int WCH = WIN / 8;                      // 150 chunks
+  constexpr int WPL = (WCH + NT - 1) / NT;          // 3 per lane
+  const bool vec_ok = ((reinterpret_cast<uintptr_t>(src) & 15) == 0);
+  auto fast = [&](int r_) {
+    const int b_ = HOP * R * r_ - N_FFT / 2;
+    return vec_ok && b_ >= 0 && b_ + WIN <= len;
+  };
+  uint4 nxt[WPL];
+  auto prefetch = [&](int r_) {
+    const uint4* s4 = reinterpret_cast<const uint4*>(src + HOP * R * r_ - N_FFT / 2);
+#pragma unroll
+    for (int j = 0; j < WPL; ++j) {
+      const int ch = lane + NT * j;
+      if (ch < WCH) nxt[j] = s4[ch];
+    }
+  };
+  if (fast(0)) prefetch(0);
+
+  for (int i = lane; i < 200; i += NT) {
+    sm.hann2[i] = cf{tb.hann2[i][0], tb.hann2[i][1]};
+    sm.tw[i / 10][i % 10] = cf{tb.tw[i / 10][i % 10][0], tb.tw[i / 10][i % 10][1]};
+  }
+  for (int i = lane; i < 101; i += NT) sm.w400[i] = cf{tb.w400k[i][0], tb.w400k[i][1]};
+  // this lane's two mel bands: first bin and the band's taps (zero past its non-zeros)
+  const int mlo = tb.mel_start[lane], mhi = tb.mel_start[lane + 64];
+  float wlo[T_LO], whi[T_HI];
+#pragma unroll
+  for (int j = 0; j < T_LO; ++j) wlo[j] = tb.mel_w[lane][j];
+#pragma unroll
+  for (int j = 0; j < T_HI; ++j) whi[j] = tb.mel_w[lane + 64][j];
+
+  FE_T_INIT
+  float smax = 0.0f, smin = INFINITY;
+  for (int r = 0; r < NR; ++r) {
+    const int f0 = r * R;
+    const int base = HOP * f0 - N_FFT / 2;
+    lds_order();   // the previous round's mel reads of st are issued
+    // ---- window: reflect padding for the STFT (centre=True, pad_mode='reflect') ------------------
+    if (fast(r)) {
+#pragma unroll
+      for (int j = 0; j < WPL; ++j) {
+        const int ch = lane + NT * j;
+        if (ch < WCH) reinterpret_cast<uint4*>(sm.win)[ch] = nxt[j];
+      }
+    } else {
+      for (int w = lane; w < WIN; w += NT) {
+        int i = base + w;
+        i = i < 0 ? -i : i;
+        i = i >= CLIP ? 2 * (CLIP - 1) - i : i;
+        sm.win[w] = i < len ? src[i] : (int16_t)0;
+      }
+    }
+    if (r + 1 < NR && fast(r + 1)) prefetch(r + 1);
+    lds_order();
+    FE_MARK(0);
+    // ---- zero crossings (edge padding, signbit semantics): lane l < 60 counts the transitions
+    //      (w - 1, w) at window positions w = 20 l .. 20 l + 19; frame f covers lanes 8 f .. 8 f + 19
+    //      minus position 160 f (its first transition is outside the frame) -------------------------
+    {
+      constexpr int ZCH = 20, ZL = WIN / ZCH;      // 60 lanes
+      static_assert(WIN % ZCH == 0 && HOP % ZCH == 0 && N_FFT % ZCH == 0, "ZCR chunking");
+      const bool interior = base >= 0 && base + WIN <= CLIP;
+      auto sgn = [&](int w) {
+        const int i = base + w;
+        return i < 0 ? sg_first : (i >= CLIP ? sg_last : (int)(sm.win[w] < 0));
+      };
+      int cl = 0, first = 0;
+      if (lane < ZL) {
+        const int w0 = ZCH * lane;
+        int prev = w0 == 0 ? -1 : (interior ? (int)(sm.win[w0 - 1] < 0) : sgn(w0 - 1));
+#pragma unroll
+        for (int j = 0; j < ZCH; ++j) {
+          const int cur = interior ? (int)(sm.win[w0 + j] < 0) : sgn(w0 + j);
+          const int x = (prev >= 0) & (cur != prev);
+          cl += x;
+          if (j == 0) first = x;
+          prev = cur;
+        }
+      }
+      int* scan = reinterpret_cast<int*>(sm.st);   // st is free until pass A writes it
+      scan[lane] = cl;
+      scan[NT + lane] = first;
+      lds_order();
+      int c = 0, fz = 0;
+      if (lane < R) {
+#pragma unroll
+        for (int l = 0; l < 20; ++l) c += scan[8 * lane + l];
+        fz = scan[NT + 8 * lane];
+      }
+      lds_order();   // scan reads are issued before pass A overwrites st
+      if (lane < R && f0 + lane < NF) sm.zc[f0 + lane] = c - fz;
+    }
+    FE_MARK(1);
+    // ---- pass A: DFT-20 over n1 of z[10 n1 + n2] (z[m] = hann-windowed (x[2m], x[2m+1])),
+    //      times W200^(n2 k1) -> st[f][k1][n2] ---------------------------------------------------------
+    if (lane < R * 10) {
+      const int f = lane / 10, n2 = lane - 10 * f;
+      const uint32_t* wp = reinterpret_cast<const uint32_t*>(sm.win) + 80 * f + n2;
+      cf u[20];
+#pragma unroll
+      for (int n1 = 0; n1 < 20; ++n1) {
+        const uint32_t w = wp[10 * n1];
+        const cf h = sm.hann2[10 * n1 + n2];
+        u[n1] = {(float)(int)(int16_t)(w & 0xffffu) * h.x, (float)((int)w >> 16) * h.y};
+      }
+      dft20(u);
+      cf* dst = &sm.st[f][n2];
+      dst[0] = u[0];
+#pragma unroll
+      for (int k1 = 1; k1 < 20; ++k1) dst[10 * k1] = cmul(u[k1], sm.tw[k1][n2]);
+    }
+    lds_order();
+    FE_MARK(2);
+    // ---- pass B: DFT-10 over n2 of row st[f][k1][*] -> Z[k1 + 20 k2], in place per frame
+    //      (frames 0-2, then 3-5: a round never reads a frame the other one writes; all of a
+    //      round's reads are issued before its writes) -------------------------------------------------
+#pragma unroll
+    for (int rr = 0; rr < 2; ++rr) {
+      if (lane < 60) {
+        const int f = 3 * rr + lane / 20, k1 = lane % 20;
+        const float4* row = reinterpret_cast<const float4*>(&sm.st[f][10 * k1]);
+        cf v[10];
+#pragma unroll
+        for (int j = 0; j < 5; ++j) {
+          const float4 q = row[j];
+          v[2 * j] = {q.x, q.y};
+          v[2 * j + 1] = {q.z, q.w};
+        }
+        lds_order();
+        dft10(v);
+#pragma unroll
+        for (int k2 = 0; k2 < 10; ++k2) sm.st[f][k1 + 20 * k2] = v[k2];
+      }
+      lds_order();
+    }
+    FE_MARK(3);
+    // ---- split: power spectrum P[f][0..200] over the frame's own Z (all reads before writes) ------
+#pragma unroll
+    for (int f = 0; f < R; ++f) {
+      const cf* Z = sm.st[f];
+      float* P = reinterpret_cast<float*>(sm.st[f]);
+      const int ka = lane, kb = lane + 64;
+      const bool hb = kb <= 100;
+      const cf za = Z[ka], zar = Z[ka == 0 ? 0 : 200 - ka], wa = sm.w400[ka];
+      cf zb = {0.f, 0.f}, zbr = {0.f, 0.f}, wb = {0.f, 0.f};
+      if (hb) {
+        zb = Z[kb];
+        zbr = Z[200 - kb];
+        wb = sm.w400[kb];
+      }
+      lds_order();
+      float p0, p1;
+      split_power(za, zar, wa, p0, p1);
+      P[ka] = p0;
+      P[200 - ka] = p1;
+      if (hb) {
+        split_power(zb, zbr, wb, p0, p1);
+        P[kb] = p0;
+        P[200 - kb] = p1;
+      }
+      lds_order();
+    }
+    FE_MARK(4);
+    // ---- mel: S[m][f] = sum_j w[m][j] P[f][start_m + j] -> 10 log10 S to the frame-major scratch ---
+    // (taps past a band's non-zeros are exact zeros times finite LDS words: same sum)
+#pragma unroll
+    for (int f = 0; f < R; ++f) {
+      if (f0 + f >= NF) break;
+      const float* P = reinterpret_cast<const float*>(sm.st[f]);
+      float a0 = 0.0f, a1 = 0.0f;
+#pragma unroll
+      for (int j = 0; j < T_LO; ++j) a0 = fmaf(wlo[j], P[mlo + j], a0);
+#pragma unroll
+      for (int j = 0; j < T_HI; ++j) a1 = fmaf(whi[j], P[mhi + j], a1);
+      float* row = scr + (f0 + f) * NMEL;
+      row[lane] = db10(a0);
+      row[lane + 64] = db10(a1);
+      smax = fmaxf(smax, fmaxf(a0, a1));
+      smin = fminf(smin, fminf(a0, a1));
+    }
+    FE_MARK(5);
+  }
+  // ---- clip max / min of the mel power (one wave: shuffles only) ----------------------------------
+  smax = wave_max(smax);
+  smin = wave_min(smin);
+  __threadfence_block();   // the scratch stores have completed: visible to this CU's re-reads
+  lds_order();
+
+  // power_to_db(ref=np.max, amin=1e-10, top_db=80) with numpy-1.21 dtypes, then normalize_matrix.
+  // log10 is monotone, so max/min of the dB matrix are the dB of max/min S.  Each numpy op rounds
+  // separately: no FMA contraction from here on.
+  {
+#pragma clang fp contract(off)
+  const float ref_db = (float)(10.0 * log10(fmax(1e-10, (double)smax)));
+  const float d_max = db10(smax) - ref_db;
+  const float thr = d_max - 80.0f;
+  const float d_min = fmaxf(db10(smin) - ref_db, thr);
+  const float diff = d_max - d_min;
+
+  float* db_out = a.db ? a.db + clip * (NMEL * NF) : nullptr;
+  float* nm_out = a.norm ? a.norm + clip * (NMEL * NF) : nullptr;
+  if (a.zcr) {
+    for (int f = lane; f < NF; f += NT) a.zcr[clip * NF + f] = (float)sm.zc[f] * (1.0f / 400.0f);
+  }
+  // LDS of the round loop is free: [151][8] tiles of normalised / dB values
+  constexpr int MB = 8;                                    // bands per column block
+  float* nvt = reinterpret_cast<float*>(sm.win);           // [NF][MB] over win + st
+  float* dbt = nvt + NF * MB;                              // [NF][MB]
+  static_assert(sizeof(sm.win) + sizeof(sm.st) >= 2 * NF * MB * sizeof(float), "LDS tiles");
+  if (a.img)
+    for (int w = lane; w < NF; w += NT) sm.rb[w] = (uint8_t)(int)(((double)sm.zc[w] / 400.0) * 255.0);
+  const float inv_diff = 1.0f / diff;
+  // the block's scratch reads are issued one block ahead (registers) so their latency hides
+  constexpr int RPL = (NF * MB / 4 + NT - 1) / NT;          // float4 per lane per block (5)
+  float4 cur[RPL], nx[RPL];
+  auto fetch = [&](int mb_, float4 (&dst)[RPL]) {
+#pragma unroll
+    for (int q = 0; q < RPL; ++q) {
+      const int i = lane + NT * q;
+      const int t = i / (MB / 4), qd = i - t * (MB / 4);
+      if (i < NF * MB / 4) dst[q] = *reinterpret_cast<const float4*>(scr + t * NMEL + MB * mb_ + 4 * qd);
+    }
+  };
+  fetch(0, nx);
+  for (int mb = 0; mb < NMEL / MB; ++mb) {
+#pragma unroll
+    for (int q = 0; q < RPL; ++q) cur[q] = nx[q];
+    if (mb + 1 < NMEL / MB) fetch(mb + 1, nx);
+    lds_order();   // the previous block's tile reads are issued
+#pragma unroll
+    for (int q = 0; q < RPL; ++q) {                           // frame t, quad of bands
+      const int i = lane + NT * q;
+      if (i >= NF * MB / 4) break;
+      const int t = i / (MB / 4), qd = i - t * (MB / 4);
+      const float pv[4] = {cur[q].x, cur[q].y, cur[q].z, cur[q].w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float d = pv[j] - ref_db;   // pv = 10 log10(max(amin, S)) from the mel pass
+        d = fmaxf(d, thr);
+        dbt[t * MB + 4 * qd + j] = d;
+        // normalize_matrix's (x - min) / (max - min) as a multiply by the reciprocal: <= 2 ulp from
+        // the division (image quantisation flips <= 1 LSB on ~1e-5 of pixels); 0 * inf = NaN
+        // keeps the digital-silence NaN
+        nvt[t * MB + 4 * qd + j] = (d - d_min) * inv_diff;
+      }
+    }
+    lds_order();
+    if (db_out || nm_out) {                                   // rows m = 8 mb .. 8 mb + 7
+      for (int e = lane; e < MB * NF; e += NT) {
+        const int rw = e / NF, t = e - rw * NF;
+        const int o = (MB * mb + rw) * NF + t;
+        if (db_out) db_out[o] = dbt[t * MB + rw];
+        if (nm_out) nm_out[o] = nvt[t * MB + rw];
+      }
+    }
+    if (a.img) {
+      // image rows h = 127 - m: the block is 8 whole rows of 453 B, word aligned
+      // R = trunc(255 * zcr[w]) (float64), G = B = trunc(255 * (1 - norm)) (float64: numpy-1.21
+      // '1 - np.float32' promotes); NaN -> 0
+      const int h_lo = NMEL - MB * (mb + 1);
+      uint32_t* out = reinterpret_cast<uint32_t*>(a.img + clip * (NMEL * NF * 3) + h_lo * NF * 3);
+      // one lane = 4 consecutive pixels of the block (row-major) = 12 bytes = 3 words
+      for (int qd = lane; qd < MB * NF / 4; qd += NT) {
+        uint32_t by[12];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int p = 4 * qd + j;
+          const int hr = p / NF, w = p - hr * NF;
+          const double v = (1.0 - (double)nvt[w * MB + (MB - 1 - hr)]) * 255.0;
+          const uint32_t gb = (v >= 0.0) ? ((uint32_t)(int)v & 255u) : 0u;   // NaN fails v >= 0
+          by[3 * j] = sm.rb[w];
+          by[3 * j + 1] = gb;
+          by[3 * j + 2] = gb;
+        }
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+          out[3 * qd + k] = by[4 * k] | (by[4 * k + 1] << 8) | (by[4 * k + 2] << 16) | (by[4 * k + 3] << 24);
+      }
+    }
+    lds_order();
+  }
+  }
+  FE_MARK(6);
+  FE_T_STORE
+}
+
+}  // namespace v2
+
+// ================================================================================================
+namespace v1 {
+
+constexpr int F = 5;             // frames per group: 25 F, 45 F, 128 F lane tasks per pass
+constexpr int NG = (NF + F - 1) / F;
+constexpr int WIN = (F - 1) * HOP + N_FFT;   // samples behind one group of frames
+
+struct Smem {                    // 15.9 KB: ~10 clips in flight per CU
+  int16_t win[WIN + 16];         // reflect-padded window of the group, base = 160 f0 - 200
+  cf t[F][9][25];                // pass 1 output, transformed in place by pass 2a
+  float pw[F][216];              // power spectrum (bins 0..200; 201.. stay 0 for the 10-tap mel dot)
+  int zc[NF + 1];                // ZCR counts of the clip
+  float hann[N_FFT];             // tables the lanes index per task (LDS, not L2 latency)
+  float w400[9][25][2];
+  float w25[5][5][2];
+};
+
+// 400-point real DFT per frame, factored n = 25*n1 + n2, k = k1 + 16*k2:
+//   pass 1 (25 tasks/frame): real 16-point DFT over n1 (via a complex 8-point FFT), k1 = 0..8,
+//                            times W400^(n2*k1)
+//   pass 2 (45 tasks/frame): 5-point DFTs over a (n2 = 5a + b), times W25^(b*c)
+//   pass 3 (45 tasks/frame): 5-point DFTs over b -> X[k1 + 16*(c + 5d)] -> |X|^2; bins > 200
+//                            fold onto 400 - k (conjugate symmetry) for k1 = 1..7
 __global__ void __launch_bounds__(NT) od_fe_kernel(OdFeArgs a) {
   __shared__ __attribute__((aligned(16))) Smem sm;
   const OdFeTables& tb = *a.tables;
@@ -108,18 +529,12 @@ __global__ void __launch_bounds__(NT) od_fe_kernel(OdFeArgs a) {
   int len = a.lens ? a.lens[clip] : a.clip_len;
   len = len < 0 ? 0 : (len > CLIP ? CLIP : len);
   const int16_t* src = a.pcm + clip * a.clip_stride;
-  // mel power of the whole clip goes to an HBM-backed scratch, frame-major [151][128] so every group
-  // stores whole 512-B frame rows; the normalisation pass re-reads it (L2/MALL-resident) in
-  // 8-band column blocks transposed through LDS
   float* scr = a.scratch + clip * (NMEL * NF);
-  // edge padding of the ZCR: samples before / after the clip repeat its first / last sample
   const int sg_first = (len > 0 ? src[0] : (int16_t)0) < 0;
   const int sg_last = (CLIP - 1 < len ? src[CLIP - 1] : (int16_t)0) < 0;
 
-  // the window of group g + 1 is loaded into registers (3 x 16 B per lane) while group g computes;
-  // groups whose window leaves [0, len) take the scalar reflect / zero-fill path instead
-  constexpr int WCH = WIN / 8;                       // 16-B chunks per window (130)
-  constexpr int WPL = (WCH + NT - 1) / NT;           // chunks per lane (3)
+  constexpr int WCH = WIN / 8;
+  constexpr int WPL = (WCH + NT - 1) / NT;
   const bool vec_ok = ((reinterpret_cast<uintptr_t>(src) & 15) == 0);
   auto fast = [&](int g_) {
     const int b_ = HOP * g_ * F - N_FFT / 2;
@@ -140,7 +555,6 @@ __global__ void __launch_bounds__(NT) od_fe_kernel(OdFeArgs a) {
   for (int i = lane; i < 9 * 25 * 2; i += NT) (&sm.w400[0][0][0])[i] = (&tb.w400[0][0][0])[i];
   for (int i = lane; i < 5 * 5 * 2; i += NT) (&sm.w25[0][0][0])[i] = (&tb.w25[0][0][0])[i];
   for (int i = lane; i < F * 216; i += NT) (&sm.pw[0][0])[i] = 0.0f;
-  // this lane's two mel bands: start bin and 10 weights (zero past the band's non-zeros)
   int mst[NMEL / NT];
   float mw[NMEL / NT][10];
 #pragma unroll
@@ -151,24 +565,12 @@ __global__ void __launch_bounds__(NT) od_fe_kernel(OdFeArgs a) {
     for (int j = 0; j < 10; ++j) mw[mh][j] = tb.mel_w[m][j];
   }
 
-#if FE_EXP
-  unsigned long long tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  unsigned long long tlast = __builtin_amdgcn_s_memtime();
-#define FE_MARK(k)                                                   \
-  do {                                                               \
-    const unsigned long long tn = __builtin_amdgcn_s_memtime();      \
-    tacc[k] += tn - tlast;                                           \
-    tlast = tn;                                                      \
-  } while (0)
-#else
-#define FE_MARK(k)
-#endif
+  FE_T_INIT
   float smax = 0.0f, smin = INFINITY;
   for (int g = 0; g < NG; ++g) {
     const int f0 = g * F;
     const int base = HOP * f0 - N_FFT / 2;
-    __syncthreads();   // the previous group is done with win / t / pw
-    // ---- window: reflect padding for the STFT (centre=True, pad_mode='reflect') ----------------
+    __syncthreads();
     if (fast(g)) {
 #pragma unroll
       for (int j = 0; j < WPL; ++j) {
@@ -186,13 +588,8 @@ __global__ void __launch_bounds__(NT) od_fe_kernel(OdFeArgs a) {
     if (g + 1 < NG && fast(g + 1)) prefetch(g + 1);
     __syncthreads();
     FE_MARK(0);
-    // ---- zero crossings of the group's frames (edge padding; transitions at padded positions
-    //      160 f + 1 .. 160 f + 399, signbit semantics) ---------------------------------------------
-    // lane l < 52 counts the transitions (w - 1, w) at window positions w = 20 l .. 20 l + 19; frame f
-    // covers lanes 8 f .. 8 f + 19 minus position 160 f (its first transition is outside the frame).
-    // Windows that touch the clip edge (edge vs reflect padding differ there) index per position.
     {
-      constexpr int ZCH = 20, ZL = WIN / ZCH;      // 52 lanes
+      constexpr int ZCH = 20, ZL = WIN / ZCH;
       static_assert(WIN % ZCH == 0 && HOP % ZCH == 0 && N_FFT % ZCH == 0, "ZCR chunking");
       const bool interior = base >= 0 && base + WIN <= CLIP;
       auto sgn = [&](int w) {
@@ -212,7 +609,7 @@ __global__ void __launch_bounds__(NT) od_fe_kernel(OdFeArgs a) {
           prev = cur;
         }
       }
-      int* scan = reinterpret_cast<int*>(sm.t);  // t is free until pass 1 writes it
+      int* scan = reinterpret_cast<int*>(sm.t);
       scan[lane] = cl;
       scan[NT + lane] = first;
       __syncthreads();
@@ -225,7 +622,6 @@ __global__ void __launch_bounds__(NT) od_fe_kernel(OdFeArgs a) {
       __syncthreads();
     }
     FE_MARK(1);
-    // ---- pass 1: real 16-point DFT over n1 of x[25 n1 + n2] * hann, times W400^(n2 k1) ----------
 #pragma unroll
     for (int r = 0; r < (F * 25 + NT - 1) / NT; ++r) {
       const int task = lane + NT * r;
@@ -245,7 +641,7 @@ __global__ void __launch_bounds__(NT) od_fe_kernel(OdFeArgs a) {
         cf zk = z[k & 7], zr = cconj(z[(8 - k) & 7]);
         cf e = cscale(cadd(zk, zr), 0.5f);
         cf d = csub(zk, zr);
-        cf o = {0.5f * d.y, -0.5f * d.x};                     // d / (2i)
+        cf o = {0.5f * d.y, -0.5f * d.x};
         cf w16 = {tb.w16[k][0], tb.w16[k][1]};
         cf y = cadd(e, cmul(w16, o));
         cf tw = {sm.w400[k][n2][0], sm.w400[k][n2][1]};
@@ -254,7 +650,6 @@ __global__ void __launch_bounds__(NT) od_fe_kernel(OdFeArgs a) {
     }
     __syncthreads();
     FE_MARK(2);
-    // ---- pass 2a: DFT-5 over a of t[k1][5a + b], times W25^(b c), in place at t[k1][5c + b] -------
 #pragma unroll
     for (int rr = 0; rr < (F * 45 + NT - 1) / NT; ++rr) {
       const int task = lane + NT * rr;
@@ -271,7 +666,6 @@ __global__ void __launch_bounds__(NT) od_fe_kernel(OdFeArgs a) {
     }
     __syncthreads();
     FE_MARK(3);
-    // ---- pass 2b: DFT-5 over b -> X[k1 + 16 (c + 5 d)] -> power; bins > 200 fold onto 400 - k ---
 #pragma unroll
     for (int rr = 0; rr < (F * 45 + NT - 1) / NT; ++rr) {
       const int task = lane + NT * rr;
@@ -292,7 +686,6 @@ __global__ void __launch_bounds__(NT) od_fe_kernel(OdFeArgs a) {
     }
     __syncthreads();
     FE_MARK(4);
-    // ---- mel: S[m][f] = sum_j w[m][j] * P[f][start_m + j] -> scratch ---------------------------------
 #pragma unroll
     for (int mh = 0; mh < NMEL / NT; ++mh) {
       const int m = lane + NT * mh;
@@ -303,7 +696,6 @@ __global__ void __launch_bounds__(NT) od_fe_kernel(OdFeArgs a) {
         float acc = 0.0f;   // the band's non-zeros in order, then exact zero terms: same result
 #pragma unroll
         for (int j = 0; j < 10; ++j) acc = fmaf(mw[mh][j], p[j], acc);
-        // power_to_db's first term, 10 log10(max(amin, S)), rounded exactly as in the epilogue
         scr[(f0 + f) * NMEL + m] = 10.0f * log10f(fmaxf(1e-10f, acc));
         smax = fmaxf(smax, acc);
         smin = fminf(smin, acc);
@@ -311,15 +703,10 @@ __global__ void __launch_bounds__(NT) od_fe_kernel(OdFeArgs a) {
     }
   }
   FE_MARK(5);
-  // ---- clip max / min of the mel power (one wave: shuffles only) ----------------------------------
   smax = wave_max(smax);
   smin = wave_min(smin);
-  __threadfence();   // the scratch stores are visible to the re-reads below (other lanes)
+  __threadfence();
   __syncthreads();
-
-  // power_to_db(ref=np.max, amin=1e-10, top_db=80) with numpy-1.21 dtypes, then normalize_matrix.
-  // log10 is monotone, so max/min of the dB matrix are the dB of max/min S.  Each numpy op rounds
-  // separately: no FMA contraction from here on.
   {
 #pragma clang fp contract(off)
   const float amin = 1e-10f;
@@ -334,17 +721,15 @@ __global__ void __launch_bounds__(NT) od_fe_kernel(OdFeArgs a) {
   if (a.zcr) {
     for (int f = lane; f < NF; f += NT) a.zcr[clip * NF + f] = (float)sm.zc[f] * (1.0f / 400.0f);
   }
-  // LDS of the group loop is free: [151][8] tiles of normalised / dB values + the R byte per column
-  constexpr int MB = 8;                                    // bands per column block
-  float* nvt = reinterpret_cast<float*>(&sm.t[0][0][0]);   // [NF][MB]
-  float* dbt = nvt + NF * MB;                               // [NF][MB]
-  uint8_t* rb = reinterpret_cast<uint8_t*>(sm.win);         // [NF]
+  constexpr int MB = 8;
+  float* nvt = reinterpret_cast<float*>(&sm.t[0][0][0]);
+  float* dbt = nvt + NF * MB;
+  uint8_t* rb = reinterpret_cast<uint8_t*>(sm.win);
   static_assert(sizeof(sm.t) + sizeof(sm.pw) >= 2 * NF * MB * sizeof(float), "LDS tiles");
   for (int w = lane; w < NF; w += NT) rb[w] = (uint8_t)(int)(((double)sm.zc[w] / 400.0) * 255.0);
   const float inv_diff = 1.0f / diff;
-  // the block's scratch reads are issued one block ahead (registers) so their latency hides
-  constexpr int RPL = (NF * MB / 4 + NT - 1) / NT;          // float4 per lane per block (5)
-  float4 cur[RPL], nxt[RPL];
+  constexpr int RPL = (NF * MB / 4 + NT - 1) / NT;
+  float4 cur[RPL], nxt2[RPL];
   auto fetch = [&](int mb_, float4 (&dst)[RPL]) {
 #pragma unroll
     for (int r = 0; r < RPL; ++r) {
@@ -353,31 +738,28 @@ __global__ void __launch_bounds__(NT) od_fe_kernel(OdFeArgs a) {
       if (i < NF * MB / 4) dst[r] = *reinterpret_cast<const float4*>(scr + t * NMEL + MB * mb_ + 4 * qd);
     }
   };
-  fetch(0, nxt);
+  fetch(0, nxt2);
   for (int mb = 0; mb < NMEL / MB; ++mb) {
 #pragma unroll
-    for (int r = 0; r < RPL; ++r) cur[r] = nxt[r];
-    if (mb + 1 < NMEL / MB) fetch(mb + 1, nxt);
+    for (int r = 0; r < RPL; ++r) cur[r] = nxt2[r];
+    if (mb + 1 < NMEL / MB) fetch(mb + 1, nxt2);
     __syncthreads();
 #pragma unroll
-    for (int r = 0; r < RPL; ++r) {                           // frame t, quad of bands
+    for (int r = 0; r < RPL; ++r) {
       const int i = lane + NT * r;
       if (i >= NF * MB / 4) break;
       const int t = i / (MB / 4), qd = i - t * (MB / 4);
       const float pv[4] = {cur[r].x, cur[r].y, cur[r].z, cur[r].w};
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        float d = pv[j] - ref_db;   // pv = 10 log10(max(amin, S)) from the mel pass
+        float d = pv[j] - ref_db;
         d = fmaxf(d, thr);
         dbt[t * MB + 4 * qd + j] = d;
-        // normalize_matrix's (x - min) / (max - min) as a multiply by the reciprocal: <= 2 ulp from
-        // the division (image quantisation flips <= 1 LSB on ~1e-5 of pixels); 0 * inf = NaN
-        // keeps the digital-silence NaN
         nvt[t * MB + 4 * qd + j] = (d - d_min) * inv_diff;
       }
     }
     __syncthreads();
-    if (db_out || nm_out) {                                   // rows m = 8 mb .. 8 mb + 7
+    if (db_out || nm_out) {
       for (int e = lane; e < MB * NF; e += NT) {
         const int r = e / NF, t = e - r * NF;
         const int o = (MB * mb + r) * NF + t;
@@ -386,12 +768,8 @@ __global__ void __launch_bounds__(NT) od_fe_kernel(OdFeArgs a) {
       }
     }
     if (a.img) {
-      // image rows h = 127 - m: the block is 8 whole rows of 453 B, word aligned
-      // R = trunc(255 * zcr[w]) (float64), G = B = trunc(255 * (1 - norm)) (float64: numpy-1.21
-      // '1 - np.float32' promotes); NaN -> 0
       const int h_lo = NMEL - MB * (mb + 1);
       uint32_t* out = reinterpret_cast<uint32_t*>(a.img + clip * (NMEL * NF * 3) + h_lo * NF * 3);
-      // one lane = 4 consecutive pixels of the block (row-major) = 12 bytes = 3 words
       for (int qd = lane; qd < MB * NF / 4; qd += NT) {
         uint32_t by[12];
 #pragma unroll
@@ -399,7 +777,7 @@ __global__ void __launch_bounds__(NT) od_fe_kernel(OdFeArgs a) {
           const int p = 4 * qd + j;
           const int hr = p / NF, w = p - hr * NF;
           const double v = (1.0 - (double)nvt[w * MB + (MB - 1 - hr)]) * 255.0;
-          const uint32_t gb = (v >= 0.0) ? ((uint32_t)(int)v & 255u) : 0u;   // NaN fails v >= 0
+          const uint32_t gb = (v >= 0.0) ? ((uint32_t)(int)v & 255u) : 0u;
           by[3 * j] = rb[w];
           by[3 * j + 1] = gb;
           by[3 * j + 2] = gb;
@@ -411,11 +789,18 @@ __global__ void __launch_bounds__(NT) od_fe_kernel(OdFeArgs a) {
     }
   }
   }
-#if FE_EXP
   FE_MARK(6);
-  if (lane == 0 && clip < 4096)
-    for (int i = 0; i < 8; ++i) g_fe_t[clip * 8 + i] = tacc[i];
-#endif
+  FE_T_STORE
+}
+
+}  // namespace v1
+
+int fe_impl() {
+  static const int impl = [] {
+    const char* e = getenv("MMLA_FE_IMPL");
+    return (e && atoi(e) == 1) ? 1 : 2;
+  }();
+  return impl;
 }
 
 }  // namespace
@@ -426,18 +811,38 @@ extern "C" int mmla_debug_fe_times(unsigned long long* host) {
 }
 #endif
 
-size_t od_fe_smem_bytes() { return sizeof(Smem); }
+size_t od_fe_smem_bytes() { return fe_impl() == 1 ? sizeof(v1::Smem) : sizeof(v2::Smem); }
+
+bool od_fe_tables_ok(const OdFeTables& t) {
+  return t.mel_taps_lo <= v2::T_LO && t.mel_taps_hi <= v2::T_HI;
+}
 
 hipError_t od_fe_launch(const OdFeArgs& a, int64_t n_clips, hipStream_t stream) {
   if (n_clips <= 0) return hipSuccess;
   if (!a.scratch) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(od_fe_kernel, dim3((unsigned)n_clips), dim3(NT), 0, stream, a);
+  if (fe_impl() == 1)
+    hipLaunchKernelGGL(v1::od_fe_kernel, dim3((unsigned)n_clips), dim3(NT), 0, stream, a);
+  else
+    hipLaunchKernelGGL(v2::od_fe_kernel, dim3((unsigned)n_clips), dim3(NT), 0, stream, a);
   return hipGetLastError();
 }
 
 void od_fe_build_tables(OdFeTables* t) {
   const double PI = 3.14159265358979323846;
   for (int n = 0; n < N_FFT; ++n) t->hann[n] = (float)(0.5 - 0.5 * cos(2.0 * PI * n / N_FFT));
+  for (int m = 0; m < 200; ++m) {   // exact power-of-two scaling of the float32 window
+    t->hann2[m][0] = t->hann[2 * m] * (1.0f / 32768.0f);
+    t->hann2[m][1] = t->hann[2 * m + 1] * (1.0f / 32768.0f);
+  }
+  for (int k1 = 0; k1 < 20; ++k1)
+    for (int n2 = 0; n2 < 10; ++n2) {
+      t->tw[k1][n2][0] = (float)cos(2.0 * PI * k1 * n2 / 200.0);
+      t->tw[k1][n2][1] = (float)-sin(2.0 * PI * k1 * n2 / 200.0);
+    }
+  for (int k = 0; k <= 100; ++k) {
+    t->w400k[k][0] = (float)cos(2.0 * PI * k / 400.0);
+    t->w400k[k][1] = (float)-sin(2.0 * PI * k / 400.0);
+  }
   for (int k = 0; k < 9; ++k) {
     t->w16[k][0] = (float)cos(2.0 * PI * k / 16.0);
     t->w16[k][1] = (float)-sin(2.0 * PI * k / 16.0);
@@ -471,6 +876,7 @@ void od_fe_build_tables(OdFeTables* t) {
     const double m = (i == NMEL + 1) ? mmax : mmin + i * step;
     mel_f[i] = mel_to_hz(m);
   }
+  t->mel_taps_lo = t->mel_taps_hi = 0;
   for (int m = 0; m < NMEL; ++m) {
     int st = -1, cnt = 0;
     float w[16] = {0};
@@ -486,12 +892,14 @@ void od_fe_build_tables(OdFeTables* t) {
       const float wv = (float)((double)v32 * enorm);
       if (wv != 0.0f) {
         if (st < 0) st = k;
-        w[k - st] = wv;
+        if (k - st < 16) w[k - st] = wv;
         cnt = k - st + 1;
       }
     }
     t->mel_start[m] = st < 0 ? 0 : st;
     t->mel_cnt[m] = cnt;
     for (int j = 0; j < 10; ++j) t->mel_w[m][j] = j < cnt ? w[j] : 0.0f;
+    int& taps = m < 64 ? t->mel_taps_lo : t->mel_taps_hi;
+    taps = cnt > taps ? cnt : taps;
   }
 }
