@@ -69,6 +69,14 @@ def load_library(path=LIB_PATH):
         if not os.path.exists(path):
             raise OSError(f'{path} not found: build it with `make -C {os.path.join(_HERE, "csrc")}` '
                           f'or `python -c "import __graft_entry__ as g; g.build()"`')
+        # PyTorch-ROCm ships its own libamdhip64.so.7 / libhsa-runtime64 (same sonames as
+        # /opt/rocm's).  The first one loaded serves the whole process; torch cannot initialise on
+        # /opt/rocm's newer runtime, while this library runs on torch's.  So when torch is present,
+        # load it first: callers may then mix libmmla and torch device buffers in either order.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         lib = ctypes.CDLL(path)
         for name, args in SIGNATURES.items():
             fn = getattr(lib, name)

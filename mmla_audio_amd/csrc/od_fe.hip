@@ -168,7 +168,7 @@ namespace v2 {
 constexpr int R = 6;                              // frames per round
 constexpr int NR = (NF + R - 1) / R;              // 26 rounds
 constexpr int WIN = (R - 1) * HOP + N_FFT;        // 1200 samples behind one round
-constexpr int T_LO = 3, T_HI = 10;                // mel taps of bands 0..63 / 64..127 (host-checked)
+constexpr int T_LO = 2, T_HI = 9;                 // mel taps of bands 0..63 / 64..127 (host-checked)
 
 struct Smem {                      // 16.8 KB
   int16_t win[WIN];                // reflect-padded window of the round, base = 160 f0 - 200
@@ -193,7 +193,10 @@ MMLA_DEV void split_power(cf z, cf zr, cf w, float& pk, float& pnk) {
   pnk = fmaf(x1.x, x1.x, x1.y * x1.y);
 }
 
-__global__ void __launch_bounds__(NT, 3) od_fe_kernel(OdFeArgs a) {
+// DB / NM / IMG: which of the dB, normalised and image outputs are written (compile-time, so the
+// epilogue's store counts are static and its waits for the scratch re-reads stay counted)
+template <bool DB, bool NM, bool IMG>
+__global__ void __launch_bounds__(NT, 2) od_fe_kernel(OdFeArgs a) {
   __shared__ __attribute__((aligned(16))) Smem sm;
   const OdFeTables& tb = *a.tables;
   const int lane = threadIdx.x;
@@ -216,16 +219,19 @@ __global__ void __launch_bounds__(NT, 3) od_fe_kernel(OdFeArgs a) {
     const int b_ = HOP * R * r_ - N_FFT / 2;
     return vec_ok && b_ >= 0 && b_ + WIN <= len;
   };
-  uint4 nxt[WPL];
-  auto prefetch = [&](int r_) {
-    const uint4* s4 = reinterpret_cast<const uint4*>(src + HOP * R * r_ - N_FFT / 2);
-#pragma unroll
-    for (int j = 0; j < WPL; ++j) {
-      const int ch = lane + NT * j;
-      if (ch < WCH) nxt[j] = s4[ch];
-    }
-  };
-  if (fast(0)) prefetch(0);
+  // three named registers (an indexed array behind a lambda was demoted to scratch memory, whose
+  // loads wait on vmcnt(0) -- i.e. on every outstanding store)
+  static_assert(WPL == 3, "window chunks per lane");
+  const bool l2 = lane < WCH - 2 * NT;              // lanes holding a third chunk
+  uint4 nx0 = {0, 0, 0, 0}, nx1 = {0, 0, 0, 0}, nx2 = {0, 0, 0, 0};
+#define FE_PREFETCH(r_)                                                                   \
+  do {                                                                                    \
+    const uint4* s4_ = reinterpret_cast<const uint4*>(src + HOP * R * (r_) - N_FFT / 2);  \
+    nx0 = s4_[lane];                                                                      \
+    nx1 = s4_[lane + NT];                                                                 \
+    nx2 = s4_[l2 ? lane + 2 * NT : WCH - 1];   /* unconditional: a static load count */   \
+  } while (0)
+  if (fast(0)) FE_PREFETCH(0);
 
   for (int i = lane; i < 200; i += NT) {
     sm.hann2[i] = cf{tb.hann2[i][0], tb.hann2[i][1]};
@@ -239,6 +245,12 @@ __global__ void __launch_bounds__(NT, 3) od_fe_kernel(OdFeArgs a) {
   for (int j = 0; j < T_LO; ++j) wlo[j] = tb.mel_w[lane][j];
 #pragma unroll
   for (int j = 0; j < T_HI; ++j) whi[j] = tb.mel_w[lane + 64][j];
+  // keep the taps in registers: without this the compiler re-loads them from global memory every
+  // round, and those loads' vmcnt waits also drain the round's outstanding scratch stores
+#pragma unroll
+  for (int j = 0; j < T_LO; ++j) asm volatile("" : "+v"(wlo[j]));
+#pragma unroll
+  for (int j = 0; j < T_HI; ++j) asm volatile("" : "+v"(whi[j]));
 
   FE_T_INIT
   float smax = 0.0f, smin = INFINITY;
@@ -248,20 +260,27 @@ __global__ void __launch_bounds__(NT, 3) od_fe_kernel(OdFeArgs a) {
     lds_order();   // the previous round's mel reads of st are issued
     // ---- window: reflect padding for the STFT (centre=True, pad_mode='reflect') ------------------
     if (fast(r)) {
-#pragma unroll
-      for (int j = 0; j < WPL; ++j) {
-        const int ch = lane + NT * j;
-        if (ch < WCH) reinterpret_cast<uint4*>(sm.win)[ch] = nxt[j];
-      }
+      uint4* w4 = reinterpret_cast<uint4*>(sm.win);
+      w4[lane] = nx0;
+      w4[lane + NT] = nx1;
+      if (l2) w4[lane + 2 * NT] = nx2;
     } else {
-      for (int w = lane; w < WIN; w += NT) {
+      // all of the lane's scalar loads are issued before the first is consumed (one wait)
+      constexpr int SPL = (WIN + NT - 1) / NT;       // 19
+      int16_t v[SPL];
+#pragma unroll
+      for (int j = 0; j < SPL; ++j) {
+        const int w = lane + NT * j;
         int i = base + w;
         i = i < 0 ? -i : i;
         i = i >= CLIP ? 2 * (CLIP - 1) - i : i;
-        sm.win[w] = i < len ? src[i] : (int16_t)0;
+        v[j] = (w < WIN && i < len) ? src[i] : (int16_t)0;
       }
+#pragma unroll
+      for (int j = 0; j < SPL; ++j)
+        if (lane + NT * j < WIN) sm.win[lane + NT * j] = v[j];
     }
-    if (r + 1 < NR && fast(r + 1)) prefetch(r + 1);
+    if (r + 1 < NR && fast(r + 1)) FE_PREFETCH(r + 1);
     lds_order();
     FE_MARK(0);
     // ---- zero crossings (edge padding, signbit semantics): lane l < 60 counts the transitions
@@ -374,16 +393,25 @@ __global__ void __launch_bounds__(NT, 3) od_fe_kernel(OdFeArgs a) {
     FE_MARK(4);
     // ---- mel: S[m][f] = sum_j w[m][j] P[f][start_m + j] -> 10 log10 S to the frame-major scratch ---
     // (taps past a band's non-zeros are exact zeros times finite LDS words: same sum)
+    // every round issues the same 12 stores (frames past the clip, last round only, repeat the
+    // round's first frame): the compiler can then count them in the next round's window wait
+    float s0 = 0.0f, s1 = 0.0f;
 #pragma unroll
     for (int f = 0; f < R; ++f) {
-      if (f0 + f >= NF) break;
       const float* P = reinterpret_cast<const float*>(sm.st[f]);
       float a0 = 0.0f, a1 = 0.0f;
 #pragma unroll
       for (int j = 0; j < T_LO; ++j) a0 = fmaf(wlo[j], P[mlo + j], a0);
 #pragma unroll
       for (int j = 0; j < T_HI; ++j) a1 = fmaf(whi[j], P[mhi + j], a1);
-      float* row = scr + (f0 + f) * NMEL;
+      if (f == 0) {
+        s0 = a0;
+        s1 = a1;
+      } else if (f0 + f >= NF) {
+        a0 = s0;
+        a1 = s1;
+      }
+      float* row = scr + min(f0 + f, NF - 1) * NMEL;
       row[lane] = db10(a0);
       row[lane + 64] = db10(a1);
       smax = fmaxf(smax, fmaxf(a0, a1));
@@ -408,76 +436,85 @@ __global__ void __launch_bounds__(NT, 3) od_fe_kernel(OdFeArgs a) {
   const float d_min = fmaxf(db10(smin) - ref_db, thr);
   const float diff = d_max - d_min;
 
-  float* db_out = a.db ? a.db + clip * (NMEL * NF) : nullptr;
-  float* nm_out = a.norm ? a.norm + clip * (NMEL * NF) : nullptr;
+  float* db_out = a.db + clip * (NMEL * NF);      // dereferenced only when DB
+  float* nm_out = a.norm + clip * (NMEL * NF);    // only when NM
   if (a.zcr) {
     for (int f = lane; f < NF; f += NT) a.zcr[clip * NF + f] = (float)sm.zc[f] * (1.0f / 400.0f);
   }
-  // LDS of the round loop is free: [151][8] tiles of normalised / dB values
+  // LDS of the round loop is free: [8][151] band-major tiles of normalised / dB values, i.e. the
+  // output layout itself (a block of 8 bands is 1208 contiguous floats of [128][151])
   constexpr int MB = 8;                                    // bands per column block
-  float* nvt = reinterpret_cast<float*>(sm.win);           // [NF][MB] over win + st
-  float* dbt = nvt + NF * MB;                              // [NF][MB]
-  static_assert(sizeof(sm.win) + sizeof(sm.st) >= 2 * NF * MB * sizeof(float), "LDS tiles");
-  if (a.img)
+  constexpr int BLK = MB * NF;                             // 1208 floats = 302 float4
+  float* nvt = reinterpret_cast<float*>(sm.win);           // [MB][NF] over win + st
+  float* dbt = nvt + BLK;                                  // [MB][NF]
+  static_assert(sizeof(sm.win) + sizeof(sm.st) >= 2 * BLK * sizeof(float), "LDS tiles");
+  static_assert(sizeof(sm.win) % 16 == 0 && BLK % 4 == 0, "16-B tile rows");
+  if (IMG)
     for (int w = lane; w < NF; w += NT) sm.rb[w] = (uint8_t)(int)(((double)sm.zc[w] / 400.0) * 255.0);
   const float inv_diff = 1.0f / diff;
-  // the block's scratch reads are issued one block ahead (registers) so their latency hides
-  constexpr int RPL = (NF * MB / 4 + NT - 1) / NT;          // float4 per lane per block (5)
+  // the block's scratch reads are issued one block ahead (registers); with static store counts the
+  // compiler's wait for them is vmcnt(N), not a drain of the previous block's output stores
+  constexpr int RPL = (BLK / 4 + NT - 1) / NT;             // float4 per lane per block (5)
   float4 cur[RPL], nx[RPL];
-  auto fetch = [&](int mb_, float4 (&dst)[RPL]) {
-#pragma unroll
-    for (int q = 0; q < RPL; ++q) {
-      const int i = lane + NT * q;
-      const int t = i / (MB / 4), qd = i - t * (MB / 4);
-      if (i < NF * MB / 4) dst[q] = *reinterpret_cast<const float4*>(scr + t * NMEL + MB * mb_ + 4 * qd);
-    }
-  };
-  fetch(0, nx);
+#define FE_FETCH(mb_)                                                                          \
+  do {                                                                                         \
+    _Pragma("unroll") for (int q_ = 0; q_ < RPL; ++q_) {                                       \
+      const int i_ = min(lane + NT * q_, BLK / 4 - 1);   /* clamped, not branched: static   */  \
+      const int t_ = i_ / (MB / 4), qd_ = i_ - t_ * (MB / 4); /* load count per block       */  \
+      nx[q_] = *reinterpret_cast<const float4*>(scr + t_ * NMEL + MB * (mb_) + 4 * qd_);       \
+    }                                                                                          \
+  } while (0)
+  FE_FETCH(0);
   for (int mb = 0; mb < NMEL / MB; ++mb) {
 #pragma unroll
     for (int q = 0; q < RPL; ++q) cur[q] = nx[q];
-    if (mb + 1 < NMEL / MB) fetch(mb + 1, nx);
+    if (mb + 1 < NMEL / MB) FE_FETCH(mb + 1);
     lds_order();   // the previous block's tile reads are issued
 #pragma unroll
     for (int q = 0; q < RPL; ++q) {                           // frame t, quad of bands
       const int i = lane + NT * q;
-      if (i >= NF * MB / 4) break;
+      if (i >= BLK / 4) break;
       const int t = i / (MB / 4), qd = i - t * (MB / 4);
       const float pv[4] = {cur[q].x, cur[q].y, cur[q].z, cur[q].w};
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         float d = pv[j] - ref_db;   // pv = 10 log10(max(amin, S)) from the mel pass
         d = fmaxf(d, thr);
-        dbt[t * MB + 4 * qd + j] = d;
+        if (DB) dbt[(4 * qd + j) * NF + t] = d;
         // normalize_matrix's (x - min) / (max - min) as a multiply by the reciprocal: <= 2 ulp from
         // the division (image quantisation flips <= 1 LSB on ~1e-5 of pixels); 0 * inf = NaN
         // keeps the digital-silence NaN
-        nvt[t * MB + 4 * qd + j] = (d - d_min) * inv_diff;
+        nvt[(4 * qd + j) * NF + t] = (d - d_min) * inv_diff;
       }
     }
     lds_order();
-    if (db_out || nm_out) {                                   // rows m = 8 mb .. 8 mb + 7
-      for (int e = lane; e < MB * NF; e += NT) {
-        const int rw = e / NF, t = e - rw * NF;
-        const int o = (MB * mb + rw) * NF + t;
-        if (db_out) db_out[o] = dbt[t * MB + rw];
-        if (nm_out) nm_out[o] = nvt[t * MB + rw];
+    if (DB || NM) {                                           // rows m = 8 mb .. 8 mb + 7
+#pragma unroll
+      for (int q = 0; q < RPL; ++q) {
+        // lanes past the block rewrite its last float4 with the same bytes: no branch around the
+        // stores, so every block issues the same number of them
+        const int e4 = min(lane + NT * q, BLK / 4 - 1);
+        if (DB) reinterpret_cast<float4*>(db_out + BLK * mb)[e4] = reinterpret_cast<const float4*>(dbt)[e4];
+        if (NM) reinterpret_cast<float4*>(nm_out + BLK * mb)[e4] = reinterpret_cast<const float4*>(nvt)[e4];
       }
     }
-    if (a.img) {
+    if (IMG) {
       // image rows h = 127 - m: the block is 8 whole rows of 453 B, word aligned
       // R = trunc(255 * zcr[w]) (float64), G = B = trunc(255 * (1 - norm)) (float64: numpy-1.21
       // '1 - np.float32' promotes); NaN -> 0
       const int h_lo = NMEL - MB * (mb + 1);
       uint32_t* out = reinterpret_cast<uint32_t*>(a.img + clip * (NMEL * NF * 3) + h_lo * NF * 3);
       // one lane = 4 consecutive pixels of the block (row-major) = 12 bytes = 3 words
-      for (int qd = lane; qd < MB * NF / 4; qd += NT) {
+#pragma unroll
+      for (int q = 0; q < RPL; ++q) {
+        const int qd = lane + NT * q;
+        if (qd >= BLK / 4) break;
         uint32_t by[12];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int p = 4 * qd + j;
           const int hr = p / NF, w = p - hr * NF;
-          const double v = (1.0 - (double)nvt[w * MB + (MB - 1 - hr)]) * 255.0;
+          const double v = (1.0 - (double)nvt[(MB - 1 - hr) * NF + w]) * 255.0;
           const uint32_t gb = (v >= 0.0) ? ((uint32_t)(int)v & 255u) : 0u;   // NaN fails v >= 0
           by[3 * j] = sm.rb[w];
           by[3 * j + 1] = gb;
@@ -488,8 +525,8 @@ __global__ void __launch_bounds__(NT, 3) od_fe_kernel(OdFeArgs a) {
           out[3 * qd + k] = by[4 * k] | (by[4 * k + 1] << 8) | (by[4 * k + 2] << 16) | (by[4 * k + 3] << 24);
       }
     }
-    lds_order();
   }
+#undef FE_FETCH
   }
   FE_MARK(6);
   FE_T_STORE
@@ -817,13 +854,28 @@ bool od_fe_tables_ok(const OdFeTables& t) {
   return t.mel_taps_lo <= v2::T_LO && t.mel_taps_hi <= v2::T_HI;
 }
 
+static void launch_v2(const OdFeArgs& a, int64_t n, hipStream_t s) {
+  const dim3 g((unsigned)n), b(NT);
+  const int k = (a.db ? 4 : 0) | (a.norm ? 2 : 0) | (a.img ? 1 : 0);
+  switch (k) {
+    case 0: hipLaunchKernelGGL((v2::od_fe_kernel<false, false, false>), g, b, 0, s, a); break;
+    case 1: hipLaunchKernelGGL((v2::od_fe_kernel<false, false, true>), g, b, 0, s, a); break;
+    case 2: hipLaunchKernelGGL((v2::od_fe_kernel<false, true, false>), g, b, 0, s, a); break;
+    case 3: hipLaunchKernelGGL((v2::od_fe_kernel<false, true, true>), g, b, 0, s, a); break;
+    case 4: hipLaunchKernelGGL((v2::od_fe_kernel<true, false, false>), g, b, 0, s, a); break;
+    case 5: hipLaunchKernelGGL((v2::od_fe_kernel<true, false, true>), g, b, 0, s, a); break;
+    case 6: hipLaunchKernelGGL((v2::od_fe_kernel<true, true, false>), g, b, 0, s, a); break;
+    default: hipLaunchKernelGGL((v2::od_fe_kernel<true, true, true>), g, b, 0, s, a); break;
+  }
+}
+
 hipError_t od_fe_launch(const OdFeArgs& a, int64_t n_clips, hipStream_t stream) {
   if (n_clips <= 0) return hipSuccess;
   if (!a.scratch) return hipErrorInvalidValue;
   if (fe_impl() == 1)
     hipLaunchKernelGGL(v1::od_fe_kernel, dim3((unsigned)n_clips), dim3(NT), 0, stream, a);
   else
-    hipLaunchKernelGGL(v2::od_fe_kernel, dim3((unsigned)n_clips), dim3(NT), 0, stream, a);
+    launch_v2(a, n_clips, stream);
   return hipGetLastError();
 }
 

@@ -10,4 +10,5 @@ for set in "SQ_WAVES SQ_INSTS_SALU SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_MFMA SQ_I
   timeout -k 10 600 rocprofv3 --pmc $set --output-format csv -d gpurun_out/pmc13_$i -o p -- python3 bench.py --workload od_features --clips 4096 --steps 1 --warmup 0 --no-cpu-baseline > gpurun_out/pmc13_$i.log 2>&1 || { echo "pass $i failed"; tail -5 gpurun_out/pmc13_$i.log; }
 done
 python3 tools/pmc_summary.py gpurun_out/pmc13_* --match od_fe > gpurun_out/pmc13_summary.txt
+rm -rf gpurun_out/pmc13_[0-9]*
 cat gpurun_out/pmc13_summary.txt
