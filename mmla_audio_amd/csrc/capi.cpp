@@ -706,6 +706,10 @@ int mmla_create(int device, mmla_ctx** out) {
   }
   SiFeTables st;
   si_fe_build_tables(&st);
+  if (!si_fe_tables_ok(st)) {   // filterbank segments exceed the front-end kernel's unrolled loops
+    mmla_destroy(c);
+    return MMLA_E_INVALID;
+  }
   if (hipMalloc(&c->od_tables, sizeof(OdFeTables)) != hipSuccess ||
       hipMalloc(&c->si_tables, sizeof(SiFeTables)) != hipSuccess ||
       hipMemcpy(c->od_tables, &ot, sizeof(ot), hipMemcpyHostToDevice) != hipSuccess ||

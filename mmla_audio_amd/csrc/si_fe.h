@@ -11,7 +11,16 @@ struct SiFeTables {
   int fb_hi[26];
   double fb_w[26][48];      // weights of filter j for bins fb_lo[j] + i
   double dct[13][26];       // ortho DCT-II rows 0..12 times the lifter (row 0 unused: log energy)
+  // v2 filterbank: segment s = bins [bin[s], bin[s+1]) (s = 0..26) is the rising edge of filter s
+  // and the falling edge of filter s-1; it is cut into sub-segments of <= 8 bins
+  int n_sub;                // number of sub-segments (<= SI_FE_MAX_SUB)
+  int sub_start[48];        // first bin of sub-segment u
+  int sub_cnt[48];          // bins in u (1..8)
+  int sub_d0[48];           // sub_start[u] - bin[s(u)]: offset of its first bin inside the segment
+  int seg_sub[28];          // sub-segments of segment s: [seg_sub[s], seg_sub[s+1])
+  double inv_w[27];         // 1 / (bin[s+1] - bin[s])
 };
+constexpr int SI_FE_MAX_SUB = 48;
 
 struct SiFeArgs {
   const int16_t* pcm;
@@ -25,4 +34,5 @@ struct SiFeArgs {
 };
 
 void si_fe_build_tables(SiFeTables* t);
+bool si_fe_tables_ok(const SiFeTables& t);
 hipError_t si_fe_launch(const SiFeArgs& a, int64_t n_blocks, hipStream_t stream);

@@ -18,3 +18,5 @@ for f in ('od', 'si', 'fe'):
     d = json.load(open(f'gpurun_out/bench_{f}.json'))
     print(f, d['value'], d['unit'], 'ms/step', round(d['ms_per_step'], 2), 'roof', {k: d['roofline'][k] for k in ('kernel', 'achieved', 'peak', 'frac') if k in d['roofline']}, 'cpu', (d.get('cpu_baseline') or {}).get('value'))
 PY
+# keep only the stats summaries (traces exceed gpurun's copy-back limit)
+find gpurun_out/prof_bench -type f ! -name '*_stats.csv' -delete

@@ -16,3 +16,5 @@ tot=sum(int(r['TotalDurationNs']) for r in mine)
 print('total ms', tot/1e6)
 for r in mine[:16]: print(f"{r['Name'][:80]:80s} {r['Calls']:>5} avg {float(r['AverageNs'])/1e6:8.3f} ms {100*int(r['TotalDurationNs'])/tot:5.1f}%")
 PY
+# keep only the stats summaries (traces exceed gpurun's copy-back limit)
+find gpurun_out/prof_tp -type f ! -name '*_stats.csv' -delete
