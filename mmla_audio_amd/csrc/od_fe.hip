@@ -170,14 +170,12 @@ constexpr int NR = (NF + R - 1) / R;              // 26 rounds
 constexpr int WIN = (R - 1) * HOP + N_FFT;        // 1200 samples behind one round
 constexpr int T_LO = 2, T_HI = 9;                 // mel taps of bands 0..63 / 64..127 (host-checked)
 
-struct Smem {                      // 16.8 KB
+struct Smem {                      // 14.4 KB
   int16_t win[WIN];                // reflect-padded window of the round, base = 160 f0 - 200
   cf st[R][200];                   // per frame: pass A out [k1][n2] -> Z[k] -> power P[k] (floats)
   int zc[NF + 1];                  // ZCR counts of the clip
   uint8_t rb[NF + 1];              // image R byte per column
-  cf hann2[200];
   cf tw[20][10];
-  cf w400[101];
 };
 static_assert(sizeof(int16_t) * WIN % 16 == 0, "st must stay 16-B aligned");
 
@@ -233,11 +231,8 @@ __global__ void __launch_bounds__(NT, 2) od_fe_kernel(OdFeArgs a) {
   } while (0)
   if (fast(0)) FE_PREFETCH(0);
 
-  for (int i = lane; i < 200; i += NT) {
-    sm.hann2[i] = cf{tb.hann2[i][0], tb.hann2[i][1]};
+  for (int i = lane; i < 200; i += NT)
     sm.tw[i / 10][i % 10] = cf{tb.tw[i / 10][i % 10][0], tb.tw[i / 10][i % 10][1]};
-  }
-  for (int i = lane; i < 101; i += NT) sm.w400[i] = cf{tb.w400k[i][0], tb.w400k[i][1]};
   // this lane's two mel bands: first bin and the band's taps (zero past its non-zeros)
   const int mlo = tb.mel_start[lane], mhi = tb.mel_start[lane + 64];
   float wlo[T_LO], whi[T_HI];
@@ -253,6 +248,17 @@ __global__ void __launch_bounds__(NT, 2) od_fe_kernel(OdFeArgs a) {
   for (int j = 0; j < T_HI; ++j) asm volatile("" : "+v"(whi[j]));
 
   FE_T_INIT
+  // split twiddles W400^k of the lane's two bins, and the pass-A window taps of its n2: per-lane
+  // constants kept in registers (LDS reads every frame / round otherwise)
+  const cf wka = {tb.w400k[lane][0], tb.w400k[lane][1]};
+  const cf wkb = lane + 64 <= 100 ? cf{tb.w400k[lane + 64][0], tb.w400k[lane + 64][1]} : cf{0.f, 0.f};
+  cf hw[20];
+  {
+    const int n2 = lane < R * 10 ? lane % 10 : 0;
+#pragma unroll
+    for (int n1 = 0; n1 < 20; ++n1) hw[n1] = cf{tb.hann2[10 * n1 + n2][0], tb.hann2[10 * n1 + n2][1]};
+  }
+
   float smax = 0.0f, smin = INFINITY;
   for (int r = 0; r < NR; ++r) {
     const int f0 = r * R;
@@ -283,29 +289,39 @@ __global__ void __launch_bounds__(NT, 2) od_fe_kernel(OdFeArgs a) {
     if (r + 1 < NR && fast(r + 1)) FE_PREFETCH(r + 1);
     lds_order();
     FE_MARK(0);
-    // ---- zero crossings (edge padding, signbit semantics): lane l < 60 counts the transitions
-    //      (w - 1, w) at window positions w = 20 l .. 20 l + 19; frame f covers lanes 8 f .. 8 f + 19
-    //      minus position 160 f (its first transition is outside the frame) -------------------------
+    // ---- zero crossings (edge padding, signbit semantics): lane l < 60 owns window positions
+    //      w = 20 l .. 20 l + 19 and counts the transitions (w - 1, w) among them from a sign-bit
+    //      mask (five 8-B LDS reads); frame f covers lanes 8 f .. 8 f + 19 minus position 160 f (its
+    //      first transition is outside the frame) --------------------------------------------------
     {
       constexpr int ZCH = 20, ZL = WIN / ZCH;      // 60 lanes
       static_assert(WIN % ZCH == 0 && HOP % ZCH == 0 && N_FFT % ZCH == 0, "ZCR chunking");
-      const bool interior = base >= 0 && base + WIN <= CLIP;
-      auto sgn = [&](int w) {
-        const int i = base + w;
-        return i < 0 ? sg_first : (i >= CLIP ? sg_last : (int)(sm.win[w] < 0));
-      };
       int cl = 0, first = 0;
       if (lane < ZL) {
         const int w0 = ZCH * lane;
-        int prev = w0 == 0 ? -1 : (interior ? (int)(sm.win[w0 - 1] < 0) : sgn(w0 - 1));
+        const uint2* wp = reinterpret_cast<const uint2*>(sm.win + w0);   // 40 B per lane
+        uint32_t m = 0;                              // bit j: signbit of window sample w0 + j
 #pragma unroll
-        for (int j = 0; j < ZCH; ++j) {
-          const int cur = interior ? (int)(sm.win[w0 + j] < 0) : sgn(w0 + j);
-          const int x = (prev >= 0) & (cur != prev);
-          cl += x;
-          if (j == 0) first = x;
-          prev = cur;
+        for (int k = 0; k < ZCH / 4; ++k) {
+          const uint2 d = wp[k];
+          // high bytes of the four samples, then their top bits gathered into a nibble
+          const uint32_t hb = __builtin_amdgcn_perm(d.y, d.x, 0x07050301u);
+          const uint32_t nib = (((hb >> 7) & 0x01010101u) * 0x01020408u) >> 24;
+          m |= (nib & 0xfu) << (4 * k);
         }
+        // bit j of e: signbit of the sample at w0 - 1 + j (j = 0..20)
+        uint32_t e = (m << 1) | (w0 > 0 ? (uint32_t)(sm.win[w0 - 1] < 0) : 0u);
+        const int i0 = base + w0 - 1;                // clip index of bit 0
+        if (i0 < 0 || i0 + ZCH >= CLIP) {            // edge padding outside the clip
+          const int nlo = min(max(-i0, 0), ZCH + 1);
+          const int jhi = min(max(CLIP - i0, 0), ZCH + 1);
+          const uint32_t lo = (1u << nlo) - 1u, hi = ((1u << (ZCH + 1)) - 1u) & ~((1u << jhi) - 1u);
+          e = (e & ~lo & ~hi) | (sg_first ? lo : 0u) | (sg_last ? hi : 0u);
+        }
+        uint32_t t = (e ^ (e >> 1)) & ((1u << ZCH) - 1u);   // bit j: transition into w0 + j
+        if (w0 == 0) t &= ~1u;                       // no sample before the window
+        cl = __builtin_popcount(t);
+        first = (int)(t & 1u);
       }
       int* scan = reinterpret_cast<int*>(sm.st);   // st is free until pass A writes it
       scan[lane] = cl;
@@ -313,8 +329,12 @@ __global__ void __launch_bounds__(NT, 2) od_fe_kernel(OdFeArgs a) {
       lds_order();
       int c = 0, fz = 0;
       if (lane < R) {
+        const int4* s4 = reinterpret_cast<const int4*>(scan + 8 * lane);
 #pragma unroll
-        for (int l = 0; l < 20; ++l) c += scan[8 * lane + l];
+        for (int l = 0; l < 5; ++l) {
+          const int4 v = s4[l];
+          c += v.x + v.y + v.z + v.w;
+        }
         fz = scan[NT + 8 * lane];
       }
       lds_order();   // scan reads are issued before pass A overwrites st
@@ -330,7 +350,7 @@ __global__ void __launch_bounds__(NT, 2) od_fe_kernel(OdFeArgs a) {
 #pragma unroll
       for (int n1 = 0; n1 < 20; ++n1) {
         const uint32_t w = wp[10 * n1];
-        const cf h = sm.hann2[10 * n1 + n2];
+        const cf h = hw[n1];
         u[n1] = {(float)(int)(int16_t)(w & 0xffffu) * h.x, (float)((int)w >> 16) * h.y};
       }
       dft20(u);
@@ -371,12 +391,12 @@ __global__ void __launch_bounds__(NT, 2) od_fe_kernel(OdFeArgs a) {
       float* P = reinterpret_cast<float*>(sm.st[f]);
       const int ka = lane, kb = lane + 64;
       const bool hb = kb <= 100;
-      const cf za = Z[ka], zar = Z[ka == 0 ? 0 : 200 - ka], wa = sm.w400[ka];
-      cf zb = {0.f, 0.f}, zbr = {0.f, 0.f}, wb = {0.f, 0.f};
+      const cf za = Z[ka], zar = Z[ka == 0 ? 0 : 200 - ka], wa = wka;
+      cf zb = {0.f, 0.f}, zbr = {0.f, 0.f};
+      const cf wb = wkb;
       if (hb) {
         zb = Z[kb];
         zbr = Z[200 - kb];
-        wb = sm.w400[kb];
       }
       lds_order();
       float p0, p1;
