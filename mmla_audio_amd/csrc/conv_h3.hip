@@ -71,8 +71,11 @@ __global__ void __launch_bounds__(NT, 2) conv_h3_kernel(ConvH3Args a) {
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave - (wave / WN) * WN;
+  // TW == 1 (Conv1D): the clips' rows form ONE sequence of n * h rows tiled 128 at a time, so a
+  // short sequence (t = 64, 32) does not pad a tile; taps that cross a clip boundary read zeros
+  const int HH = TW == 1 ? a.n * a.h : a.h;
   const int tiles = a.tiles_h * a.tiles_w;
-  const int64_t clip = blockIdx.x / tiles;
+  const int64_t clip = TW == 1 ? 0 : blockIdx.x / tiles;
   const int tile = blockIdx.x - (int)(clip * tiles);
   const int th_i = tile / a.tiles_w;
   const int h0 = th_i * TH;
@@ -85,6 +88,9 @@ __global__ void __launch_bounds__(NT, 2) conv_h3_kernel(ConvH3Args a) {
     const int m = (wm * MT + mt) * 32 + (lane & 31);
     apix[mt] = ((m / TW) * WP + (m % TW)) * LDP;
   }
+  int trow[MT];   // TW == 1: the A row's position inside its clip
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) trow[mt] = (h0 + (wm * MT + mt) * 32 + (lane & 31)) % a.h;
   const int koff = (lane >> 5) * 8;
 
   f32x16 acc1[MT][NTL], acc2[MT][NTL];
@@ -107,7 +113,7 @@ __global__ void __launch_bounds__(NT, 2) conv_h3_kernel(ConvH3Args a) {
     wlp[nt] = a.wl + (size_t)co * a.cin_pad + koff;
   }
   const size_t tap_stride = (size_t)a.cout_pad * a.cin_pad;
-  const float* xclip = a.x + clip * a.h * a.w * a.cin;
+  const float* xclip = a.x + clip * HH * a.w * a.cin;
 
   const int nchunks = a.cin_pad / CK;
   for (int ch = 0; ch < nchunks; ++ch) {
@@ -128,7 +134,7 @@ __global__ void __launch_bounds__(NT, 2) conv_h3_kernel(ConvH3Args a) {
         const int py = px / WP, pxx = px % WP;
         const int ih = h0 - a.pad_h + py, iw = w0 - a.pad_w + pxx;
         const int ci = ci0 + q * 4;
-        if (ih >= 0 && ih < a.h && iw >= 0 && iw < a.w && ci < a.cin) {
+        if (ih >= 0 && ih < HH && iw >= 0 && iw < a.w && ci < a.cin) {
           pre[j] = *reinterpret_cast<const float4*>(xclip + (ih * a.w + iw) * a.cin + ci);
           valid |= 1u << j;
         }
@@ -195,8 +201,15 @@ __global__ void __launch_bounds__(NT, 2) conv_h3_kernel(ConvH3Args a) {
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
           const int off = apix[mt] + toff + 16 * s + koff;
-          const f16x8 ah = *reinterpret_cast<const f16x8*>(lds_hi + off);
-          const f16x8 al = *reinterpret_cast<const f16x8*>(lds_lo + off);
+          f16x8 ah = *reinterpret_cast<const f16x8*>(lds_hi + off);
+          f16x8 al = *reinterpret_cast<const f16x8*>(lds_lo + off);
+          if constexpr (TW == 1 && KH > 1) {
+            const int src = trow[mt] + dy - a.pad_h;
+            if (src < 0 || src >= a.h) {
+              ah = f16x8{};
+              al = f16x8{};
+            }
+          }
 #pragma unroll
           for (int nt = 0; nt < NTL; ++nt) {
             acc1[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[nt][s], acc1[mt][nt], 0, 0, 0);
@@ -260,16 +273,16 @@ __global__ void __launch_bounds__(NT, 2) conv_h3_kernel(ConvH3Args a) {
         for (int g = 0; g < 4; ++g) {        // 4 groups of 4 consecutive tile rows
           const int m0 = mbase + 8 * g + hsel;
           const int oh = h0 + m0 / TW;
-          if (oh >= a.h) continue;
+          if (oh >= HH) continue;
           const int ow0 = w0 + m0 % TW;
-          float* yp = a.y + ((clip * a.h + oh) * a.w + ow0) * a.cout + co;
+          float* yp = a.y + ((clip * HH + oh) * a.w + ow0) * a.cout + co;
           const float* rp = nullptr;
-          if constexpr (EPI == EPI_ADD) rp = a.res + ((clip * a.h + oh) * a.w + ow0) * a.cout + co;
+          if constexpr (EPI == EPI_ADD) rp = a.res + ((clip * HH + oh) * a.w + ow0) * a.cout + co;
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             // TW >= 4 keeps the 4 rows in one image row; TW == 1 walks image rows instead
             const int step = TW == 1 ? a.w * a.cout : a.cout;
-            const bool ok = TW == 1 ? (oh + j < a.h) : (ow0 + j < a.w);
+            const bool ok = TW == 1 ? (oh + j < HH) : (ow0 + j < a.w);
             if (!ok) continue;
             float val = v[4 * g + j];
             if constexpr (EPI == EPI_ADD) val += rp[j * step];
@@ -283,7 +296,8 @@ __global__ void __launch_bounds__(NT, 2) conv_h3_kernel(ConvH3Args a) {
 
 template <int KH, int KW, int CK, int BN, int TW, int PRO, int EPI, bool POOL>
 hipError_t launch(const ConvH3Args& a, hipStream_t s) {
-  dim3 grid((unsigned)((int64_t)a.n * a.tiles_h * a.tiles_w), (unsigned)(a.cout_pad / BN));
+  const int64_t tiles = (int64_t)a.tiles_h * a.tiles_w * (TW == 1 ? 1 : a.n);
+  dim3 grid((unsigned)tiles, (unsigned)(a.cout_pad / BN));
   hipLaunchKernelGGL((conv_h3_kernel<KH, KW, CK, BN, TW, PRO, EPI, POOL>), grid, dim3(NT), 0, s, a);
   return hipGetLastError();
 }
@@ -303,7 +317,8 @@ hipError_t conv_h3_launch(ConvH3Args a, hipStream_t s) {
   // tile: 16 wide for wide images, 8 for narrow ones (W = 38, 19), 1 for Conv1D
   a.tw = a.w == 1 ? 1 : (a.w >= 48 ? 16 : 8);
   a.th = BM / a.tw;
-  a.tiles_h = (a.h + a.th - 1) / a.th;
+  // Conv1D: one row sequence over all clips (conv_h3_kernel TW == 1)
+  a.tiles_h = a.tw == 1 ? (int)(((int64_t)a.n * a.h + a.th - 1) / a.th) : (a.h + a.th - 1) / a.th;
   a.tiles_w = (a.w + a.tw - 1) / a.tw;
   const int ck = a.cin_pad % 32 == 0 ? 32 : 16;
   if (a.cin_pad % ck != 0) return hipErrorInvalidValue;
