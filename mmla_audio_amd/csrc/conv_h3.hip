@@ -233,6 +233,31 @@ __global__ void __launch_bounds__(NT, 2) conv_h3_kernel(ConvH3Args a) {
   // ---- epilogue ----------------------------------------------------------------------------------
   // lane's accumulator register r holds tile row m = mbase + (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
   const int hsel = 4 * (lane >> 5);
+  // the residual is added in place (res == y): all of the lane's residual loads are issued before
+  // its first store, otherwise every load waits behind the previous (possibly aliasing) store
+  float rsd[NTL][MT][16];
+  if constexpr (EPI == EPI_ADD && !POOL) {
+#pragma unroll
+    for (int nt = 0; nt < NTL; ++nt) {
+      const int co = n0 + (wn * NTL + nt) * 32 + (lane & 31);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const int mbase = (wm * MT + mt) * 32;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int m0 = mbase + 8 * g + hsel;
+          const int oh = h0 + m0 / TW, ow0 = w0 + m0 % TW;
+          const float* rp = a.res + ((clip * HH + oh) * a.w + ow0) * a.cout + co;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int step = TW == 1 ? a.w * a.cout : a.cout;
+            const bool ok = co < a.cout && oh < HH && (TW == 1 ? (oh + j < HH) : (ow0 + j < a.w));
+            rsd[nt][mt][4 * g + j] = ok ? rp[j * step] : 0.0f;
+          }
+        }
+      }
+    }
+  }
 #pragma unroll
   for (int nt = 0; nt < NTL; ++nt) {
     const int co = n0 + (wn * NTL + nt) * 32 + (lane & 31);
@@ -276,8 +301,6 @@ __global__ void __launch_bounds__(NT, 2) conv_h3_kernel(ConvH3Args a) {
           if (oh >= HH) continue;
           const int ow0 = w0 + m0 % TW;
           float* yp = a.y + ((clip * HH + oh) * a.w + ow0) * a.cout + co;
-          const float* rp = nullptr;
-          if constexpr (EPI == EPI_ADD) rp = a.res + ((clip * HH + oh) * a.w + ow0) * a.cout + co;
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             // TW >= 4 keeps the 4 rows in one image row; TW == 1 walks image rows instead
@@ -285,7 +308,7 @@ __global__ void __launch_bounds__(NT, 2) conv_h3_kernel(ConvH3Args a) {
             const bool ok = TW == 1 ? (oh + j < HH) : (ow0 + j < a.w);
             if (!ok) continue;
             float val = v[4 * g + j];
-            if constexpr (EPI == EPI_ADD) val += rp[j * step];
+            if constexpr (EPI == EPI_ADD) val += rsd[nt][mt][4 * g + j];
             yp[j * step] = val;
           }
         }
