@@ -157,7 +157,21 @@ __global__ void __launch_bounds__(NT) conv_kernel(ConvArgs a) {
     }
   }
 
-  // epilogue: acc register r of lane holds row (r&3) + 8(r>>2) + 4(lane>>5), column lane&31
+  // epilogue: acc register r of lane holds row (r&3) + 8(r>>2) + 4(lane>>5), column lane&31.
+  // All residual loads are issued before the first store (y and res may alias: interleaved, each
+  // load would wait behind the previous store)
+  float rsd[BN / 32][16];
+  if constexpr (EPI == EPI_ADD) {
+#pragma unroll
+    for (int t = 0; t < BN / 32; ++t) {
+      const int co = n0 + t * 32 + (lane & 31);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t p = p0 + wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        rsd[t][r] = (co < a.cout && p < P) ? a.res[p * a.cout + co] : 0.0f;
+      }
+    }
+  }
 #pragma unroll
   for (int t = 0; t < BN / 32; ++t) {
     const int co = n0 + t * 32 + (lane & 31);
@@ -170,7 +184,7 @@ __global__ void __launch_bounds__(NT) conv_kernel(ConvArgs a) {
       if (p >= P) continue;
       float v = acc[t][r] + b;
       if constexpr (EPI == EPI_ADD) {
-        v += a.res[p * a.cout + co];
+        v += rsd[t][r];
       } else if constexpr (EPI == EPI_ADD_POOL) {
         const int hw = a.ho * a.wo;
         const int n = (int)(p / hw);
