@@ -4,7 +4,7 @@
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-for wl in od_pipeline od_features; do
+for wl in od_pipeline od_features si_pipeline; do
   for ctr in FETCH_SIZE WRITE_SIZE; do
     rm -rf gpurun_out/pmct_${wl}_$ctr
     timeout -k 10 600 rocprofv3 --pmc $ctr --output-format csv -d gpurun_out/pmct_${wl}_$ctr -o p -- python3 bench.py --workload $wl --steps 1 --warmup 0 --no-cpu-baseline > gpurun_out/pmct_${wl}_$ctr.log 2>&1 || exit $?

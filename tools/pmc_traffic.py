@@ -48,8 +48,9 @@ def main():
               'read_bytes_per_launch': v['read_bytes'] / max(v['dispatches'], 1),
               'write_bytes_per_launch': v['write_bytes'] / max(v['dispatches'], 1)}
           for s, v in stages.items()}
-    # clips each launch processed: the library's OD micro-batch (4096) / the od_features bench batch
-    cpl = {s: 4096 for s in st}
+    # clips each launch processed: the library's micro-batch (OD 4096, SI 16384) / the od_features
+    # bench batch (4096)
+    cpl = {s: (16384 if wl == 'si_pipeline' else 4096) for s in st}
     json.dump({'workload': wl, 'clips_per_launch': cpl, 'note': 'rocprofv3 --pmc FETCH_SIZE (x2, gfx950) and WRITE_SIZE in '
                'separate passes over `bench.py --workload %s --steps 1 --warmup 0`' % wl,
                'stages': st, 'kernels': kernels}, sys.stdout, indent=1)
