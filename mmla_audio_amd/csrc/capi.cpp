@@ -250,7 +250,9 @@ int take_conv(mmla_ctx* c, Cursor& cur, std::vector<void*>& al, int kh, int kw, 
   memcpy(bp.data(), b, sizeof(float) * cout);
   CHK(upload(c, al, kp.data(), kp.size() * sizeof(float), &w->wt));
   CHK(upload(c, al, bp.data(), bp.size() * sizeof(float), &w->bias));
-  if (kh * kw > 1 && cin % 4 == 0) {   // spatial conv: also the 3xFP16 operand layout
+  // spatial conv: also the 3xFP16 operand layout (cin % 4 != 0: only the SI stem's 4-tap Conv1D,
+  // conv_h3.hip stages it element-wise)
+  if (kh * kw > 1 && (cin % 4 == 0 || (kh == 4 && kw == 1 && cout <= 32))) {
     w->cin_pad = (cin + 15) / 16 * 16;
     const size_t n = (size_t)kh * kw * w->cout_pad * w->cin_pad;
     std::vector<uint16_t> hi(n), lo(n);
@@ -619,7 +621,7 @@ int run_si_net(mmla_ctx* c, const float* x, int64_t n, float* probs, int32_t* ar
   float* R = static_cast<float*>(pt3);
   int t = SI_T;
   // Conv1D(32, 4, same): [n, 256, 1, 39] -> [n, 256, 1, 32] (speaker_identification.py:195)
-  CHK(conv_run(c, conv_args(W.stem, x, X, (int)n, t, 1, 1, nullptr, PRO_NONE, EPI_BIAS, nullptr)));
+  CHK(conv_spatial(c, W.stem, x, X, (int)n, t, 1, nullptr, PRO_NONE, EPI_BIAS, nullptr));
   for (int u = 0; u < 9; ++u) {   // res_unit, speaker_identification.py:168-190
     const SiUnit& U = W.unit[u];
     const int cin = U.ca.cin;

@@ -50,7 +50,8 @@ MMLA_DEV float pro_fn(float v, float sc, float sh) {
   }
 }
 
-template <int KH, int KW, int CK, int BN, int TW, int PRO, int EPI, bool POOL>
+// V4: channels loaded as float4 (cin % 4 == 0); else per element (the SI stem, cin = 39)
+template <int KH, int KW, int CK, int BN, int TW, int PRO, int EPI, bool POOL, bool V4 = true>
 __global__ void __launch_bounds__(NT, 2) conv_h3_kernel(ConvH3Args a) {
   // each wave owns ONE 32-column slice of B (no B fragment is loaded by two waves) and
   // 128 / WM rows: BN 32 -> 4 x 1, BN 64 -> 2 x 2, BN 128 -> 1 x 4 (waves along N)
@@ -135,7 +136,15 @@ __global__ void __launch_bounds__(NT, 2) conv_h3_kernel(ConvH3Args a) {
         const int ih = h0 - a.pad_h + py, iw = w0 - a.pad_w + pxx;
         const int ci = ci0 + q * 4;
         if (ih >= 0 && ih < HH && iw >= 0 && iw < a.w && ci < a.cin) {
-          pre[j] = *reinterpret_cast<const float4*>(xclip + (ih * a.w + iw) * a.cin + ci);
+          const float* src = xclip + (ih * a.w + iw) * a.cin + ci;
+          if constexpr (V4) {
+            pre[j] = *reinterpret_cast<const float4*>(src);
+          } else {
+            pre[j].x = src[0];
+            pre[j].y = ci + 1 < a.cin ? src[1] : 0.0f;
+            pre[j].z = ci + 2 < a.cin ? src[2] : 0.0f;
+            pre[j].w = ci + 3 < a.cin ? src[3] : 0.0f;
+          }
           valid |= 1u << j;
         }
       }
@@ -317,11 +326,11 @@ __global__ void __launch_bounds__(NT, 2) conv_h3_kernel(ConvH3Args a) {
   }
 }
 
-template <int KH, int KW, int CK, int BN, int TW, int PRO, int EPI, bool POOL>
+template <int KH, int KW, int CK, int BN, int TW, int PRO, int EPI, bool POOL, bool V4 = true>
 hipError_t launch(const ConvH3Args& a, hipStream_t s) {
   const int64_t tiles = (int64_t)a.tiles_h * a.tiles_w * (TW == 1 ? 1 : a.n);
   dim3 grid((unsigned)tiles, (unsigned)(a.cout_pad / BN));
-  hipLaunchKernelGGL((conv_h3_kernel<KH, KW, CK, BN, TW, PRO, EPI, POOL>), grid, dim3(NT), 0, s, a);
+  hipLaunchKernelGGL((conv_h3_kernel<KH, KW, CK, BN, TW, PRO, EPI, POOL, V4>), grid, dim3(NT), 0, s, a);
   return hipGetLastError();
 }
 
@@ -336,7 +345,19 @@ hipError_t by_bn(const ConvH3Args& a, hipStream_t s) {
 
 hipError_t conv_h3_launch(ConvH3Args a, hipStream_t s) {
   if ((int64_t)a.n * a.h * a.w == 0) return hipSuccess;
-  if (a.cin % 4 != 0 || a.cout_pad % 32 != 0) return hipErrorInvalidValue;
+  if (a.cout_pad % 32 != 0) return hipErrorInvalidValue;
+  // SI stem Conv1D(32, 4, same) on the [t, 39] features: element-wise staging, cin_pad 48
+  if (a.cin % 4 != 0) {
+    if (a.kh == 4 && a.kw == 1 && a.w == 1 && a.cin_pad % 16 == 0 && a.cout_pad == 32 &&
+        a.pro == PRO_NONE && a.epi == EPI_BIAS && !a.pool_out) {
+      a.tw = 1;
+      a.th = BM;
+      a.tiles_h = (int)(((int64_t)a.n * a.h + a.th - 1) / a.th);
+      a.tiles_w = 1;
+      return launch<4, 1, 16, 32, 1, PRO_NONE, EPI_BIAS, false, false>(a, s);
+    }
+    return hipErrorInvalidValue;
+  }
   // tile: 16 wide for wide images, 8 for narrow ones (W = 38, 19), 1 for Conv1D
   a.tw = a.w == 1 ? 1 : (a.w >= 48 ? 16 : 8);
   a.th = BM / a.tw;
