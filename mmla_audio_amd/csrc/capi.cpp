@@ -43,6 +43,8 @@ struct BnW {
 struct LstmW {
   float* wcat[2] = {nullptr, nullptr};
   float* bias[2] = {nullptr, nullptr};
+  uint16_t* wth[2] = {nullptr, nullptr};   // 3xFP16 split, transposed [1024][256 + D] (nets.hip)
+  uint16_t* wtl[2] = {nullptr, nullptr};
 };
 struct OdBlock {
   BnW bn_in, bn_mid;
@@ -306,6 +308,13 @@ int take_lstm(mmla_ctx* c, Cursor& cur, std::vector<void*>& al, int d, LstmW* l)
     memcpy(wc.data() + 256 * 1024, k, sizeof(float) * d * 1024);
     CHK(upload(c, al, wc.data(), wc.size() * sizeof(float), &l->wcat[dir]));
     CHK(upload(c, al, b, 1024 * sizeof(float), &l->bias[dir]));
+    std::vector<uint16_t> hi(wc.size()), lo(wc.size());
+    bilstm_h3_split_weights(wc.data(), d, hi.data(), lo.data());
+    float* p = nullptr;
+    CHK(upload(c, al, hi.data(), hi.size() * sizeof(uint16_t), &p));
+    l->wth[dir] = reinterpret_cast<uint16_t*>(p);
+    CHK(upload(c, al, lo.data(), lo.size() * sizeof(uint16_t), &p));
+    l->wtl[dir] = reinterpret_cast<uint16_t*>(p);
   }
   return MMLA_OK;
 }
@@ -470,6 +479,15 @@ int conv_spatial(mmla_ctx* c, const ConvW& w, const float* x, float* y, int n, i
 
 double lstm_flops(int64_t n, int T, int D) { return 2.0 * n * T * 2 * (256.0 + D) * 1024.0; }
 
+// BiLSTM on the 3xFP16 path when enabled (exact-f32 MFMA kernel otherwise)
+hipError_t lstm_run(mmla_ctx* c, const LstmW& L, const float* seq, int64_t n, int T, float* out) {
+  if (c->precision == MMLA_PREC_F16X3 && L.wth[0])
+    return bilstm_h3_launch(seq, (int)n, T, 128, L.wth[0], L.wtl[0], L.wth[1], L.wtl[1], L.bias[0],
+                            L.bias[1], out, c->stream);
+  return bilstm_launch(seq, (int)n, T, 128, L.wcat[0], L.wcat[1], L.bias[0], L.bias[1], out,
+                       c->stream);
+}
+
 // OD-NET on a device batch; input = uint8 image (img_u8) or float NHWC (img_f32).
 // `stop` >= 0 (debug trace): return after stage `stop` (0 stem, 1..9 res blocks, 10 mean, 11
 // BiLSTM) with *tap / *tap_n set to that stage's output tensor.
@@ -590,8 +608,7 @@ int run_od_net(mmla_ctx* c, const uint8_t* img_u8, const float* img_f32, int64_t
     return MMLA_OK;
   }
   LAUNCH(c, MMLA_STAGE_LSTM, lstm_flops(n, w, 128),
-         bilstm_launch(static_cast<float*>(pseq), (int)n, w, 128, W.lstm.wcat[0], W.lstm.wcat[1],
-                       W.lstm.bias[0], W.lstm.bias[1], static_cast<float*>(ph), c->stream));
+         lstm_run(c, W.lstm, static_cast<float*>(pseq), n, w, static_cast<float*>(ph)));
   if (stop == 11) {
     *tap = static_cast<float*>(ph);
     *tap_n = n * 512;
@@ -644,9 +661,7 @@ int run_si_net(mmla_ctx* c, const float* x, int64_t n, float* probs, int32_t* ar
          bn_relu_avgpool4_launch(X, (int)n, t, 128, W.final_bn.scale, W.final_bn.shift,
                                  static_cast<float*>(pseq), c->stream));
   LAUNCH(c, MMLA_STAGE_LSTM, lstm_flops(n, t / 4, 128),
-         bilstm_launch(static_cast<float*>(pseq), (int)n, t / 4, 128, W.lstm.wcat[0],
-                       W.lstm.wcat[1], W.lstm.bias[0], W.lstm.bias[1], static_cast<float*>(ph),
-                       c->stream));
+         lstm_run(c, W.lstm, static_cast<float*>(pseq), n, t / 4, static_cast<float*>(ph)));
   ConvArgs d = conv_args(W.dense, static_cast<float*>(ph), static_cast<float*>(pl), (int)n, 1, 1, 1,
                          nullptr, PRO_NONE, EPI_BIAS, nullptr);
   d.ldy = W.dense.cout_pad;

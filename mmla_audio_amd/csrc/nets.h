@@ -20,6 +20,12 @@ hipError_t bn_relu_avgpool4_launch(const float* x, int n, int t, int c, const fl
 hipError_t bilstm_launch(const float* seq, int n, int T, int D, const float* wcat_fwd,
                          const float* wcat_bwd, const float* bias_fwd, const float* bias_bwd,
                          float* out, hipStream_t s);
+// The same BiLSTM on the f16 MFMA with 3xFP16 products (error-compensated hi/lo splits, f32
+// accumulation); w*h / w*l = bilstm_h3_split_weights(wcat): [1024][256 + D] fp16 bits.
+hipError_t bilstm_h3_launch(const float* seq, int n, int T, int D, const uint16_t* wfh,
+                            const uint16_t* wfl, const uint16_t* wbh, const uint16_t* wbl,
+                            const float* bias_fwd, const float* bias_bwd, float* out, hipStream_t s);
+void bilstm_h3_split_weights(const float* wcat, int D, uint16_t* hi, uint16_t* lo);
 // OD head: LeakyReLU(0.3) -> Dense(512 -> 2) -> softmax; probs [n,2], argmax [n] (nullable)
 hipError_t od_head_launch(const float* h, int n, const float* w /*[512][2]*/, const float* b,
                           float* probs, int32_t* argmax, hipStream_t s);

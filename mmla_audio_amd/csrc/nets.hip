@@ -9,6 +9,8 @@
 #include "common.h"
 #include "nets.h"
 
+#include <cstring>
+
 namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -168,6 +170,132 @@ __global__ void __launch_bounds__(256) bilstm_kernel(const float* __restrict__ s
   }
 }
 
+
+// ---- 3xFP16 BiLSTM ----------------------------------------------------------------------------
+// The same recurrence with the [32 x 384] x [384 x 1024] step product on the f16 MFMA
+// (v_mfma_f32_32x32x16_f16) as error-compensated 3xFP16 (conv_h3.hip): A = [h_{t-1} | x_t] split
+// into fp16 hi/lo in LDS, B = the stacked kernels pre-split on the host and TRANSPOSED to
+// [1024 gate columns][384 k] so a lane's 8 k-values are one 16-B load.  Eight waves: wave w owns
+// hidden units [32w, 32w + 32) of all four gates (4 accumulator tiles x {hi*hi, hi*lo + lo*hi}), so
+// the gate math and the c-state stay in registers as in the f32 kernel.
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+constexpr float LSTM_LO = 2048.0f;
+
+// gate nonlinearities on the hardware exp / rcp (a few ulp from expf / tanhf; far inside the 1e-4
+// probability tolerance) -- fewer registers live beside the 128 accumulators
+MMLA_DEV float sigm_f(float z) { return __frcp_rn(1.0f + __expf(-z)); }
+MMLA_DEV float tanh_f(float x) { return 1.0f - 2.0f * __frcp_rn(1.0f + __expf(2.0f * x)); }
+
+MMLA_DEV void split1(float v, _Float16& h, _Float16& l) {
+  h = (_Float16)v;
+  l = (_Float16)((v - (float)h) * LSTM_LO);
+}
+
+template <int D>
+__global__ void __launch_bounds__(512) bilstm_h3_kernel(const float* __restrict__ seq, int n, int T,
+                                                        const uint16_t* __restrict__ wfh,
+                                                        const uint16_t* __restrict__ wfl,
+                                                        const uint16_t* __restrict__ wbh,
+                                                        const uint16_t* __restrict__ wbl,
+                                                        const float* __restrict__ bf,
+                                                        const float* __restrict__ bb,
+                                                        float* __restrict__ out) {
+  constexpr int K = LSTM_U + D;          // 384
+  constexpr int LDA = K + 8;             // fp16 per A row (16-B pad)
+  constexpr int NTH = 512;
+  __shared__ __attribute__((aligned(16))) _Float16 Ahi[LSTM_ROWS * LDA];
+  __shared__ __attribute__((aligned(16))) _Float16 Alo[LSTM_ROWS * LDA];
+  __shared__ float Cs[LSTM_ROWS * LSTM_U];   // c-state (registers are taken by the accumulators)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int dir = blockIdx.y;
+  const uint16_t* __restrict__ Wh = dir == 0 ? wfh : wbh;
+  const uint16_t* __restrict__ Wl = dir == 0 ? wfl : wbl;
+  const float* __restrict__ B = dir == 0 ? bf : bb;
+  const int64_t c0 = (int64_t)blockIdx.x * LSTM_ROWS;
+
+  for (int e = tid; e < LSTM_ROWS * LSTM_U; e += NTH) {   // h_{-1} = 0
+    Ahi[(e / LSTM_U) * LDA + e % LSTM_U] = (_Float16)0.0f;
+    Alo[(e / LSTM_U) * LDA + e % LSTM_U] = (_Float16)0.0f;
+  }
+  const int col = 32 * wave + (lane & 31);   // hidden unit of this lane's accumulator column
+  const int koff = 8 * (lane >> 5);
+  float bias[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) bias[g] = B[g * LSTM_U + col];
+  const uint16_t* wh[4];
+  const uint16_t* wl[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    wh[g] = Wh + (size_t)(g * LSTM_U + col) * K + koff;
+    wl[g] = Wl + (size_t)(g * LSTM_U + col) * K + koff;
+  }
+  const _Float16* arow_h = Ahi + (lane & 31) * LDA + koff;
+  const _Float16* arow_l = Alo + (lane & 31) * LDA + koff;
+  for (int e = tid; e < LSTM_ROWS * LSTM_U; e += NTH) Cs[e] = 0.0f;
+
+  for (int s = 0; s < T; ++s) {
+    const int t = dir == 0 ? s : T - 1 - s;
+    // x_t -> A[:, 256:256+D] (float4 loads, split once)
+    for (int e = tid; e < LSTM_ROWS * D / 4; e += NTH) {
+      const int r = e / (D / 4), d4 = e - r * (D / 4);
+      const int64_t clip = c0 + r;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (clip < n) v = *reinterpret_cast<const float4*>(seq + (clip * T + t) * D + 4 * d4);
+      _Float16 h0, h1, h2, h3, l0, l1, l2, l3;
+      split1(v.x, h0, l0);
+      split1(v.y, h1, l1);
+      split1(v.z, h2, l2);
+      split1(v.w, h3, l3);
+      const f16x4 hv = {h0, h1, h2, h3}, lv = {l0, l1, l2, l3};
+      *reinterpret_cast<f16x4*>(Ahi + r * LDA + LSTM_U + 4 * d4) = hv;
+      *reinterpret_cast<f16x4*>(Alo + r * LDA + LSTM_U + 4 * d4) = lv;
+    }
+    __syncthreads();
+    f32x16 a1[4], a2[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        a1[g][r] = bias[g];
+        a2[g][r] = 0.0f;
+      }
+#pragma unroll 1
+    for (int ks = 0; ks < K / 16; ++ks) {
+      const f16x8 ah = *reinterpret_cast<const f16x8*>(arow_h + 16 * ks);
+      const f16x8 al = *reinterpret_cast<const f16x8*>(arow_l + 16 * ks);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const f16x8 bh = *reinterpret_cast<const f16x8*>(wh[g] + 16 * ks);
+        const f16x8 bl = *reinterpret_cast<const f16x8*>(wl[g] + 16 * ks);
+        a1[g] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, a1[g], 0, 0, 0);
+        a2[g] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, a2[g], 0, 0, 0);
+        a2[g] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, a2[g], 0, 0, 0);
+      }
+    }
+    __syncthreads();   // every wave has read h_{t-1}
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      const float ig = sigm_f(a1[0][r] + a2[0][r] * (1.0f / LSTM_LO));
+      const float fg = sigm_f(a1[1][r] + a2[1][r] * (1.0f / LSTM_LO));
+      const float gg = tanh_f(a1[2][r] + a2[2][r] * (1.0f / LSTM_LO));
+      const float og = sigm_f(a1[3][r] + a2[3][r] * (1.0f / LSTM_LO));
+      const float c = fg * Cs[row * LSTM_U + col] + ig * gg;
+      Cs[row * LSTM_U + col] = c;
+      const float h = og * tanh_f(c);
+      if (s == T - 1) {   // the last state (Keras return_sequences=False), float32
+        const int64_t clip = c0 + row;
+        if (clip < n) out[clip * 512 + dir * LSTM_U + col] = h;
+      }
+      _Float16 hh, hl;
+      split1(h, hh, hl);
+      Ahi[row * LDA + col] = hh;
+      Alo[row * LDA + col] = hl;
+    }
+  }
+}
+
 __global__ void od_head_kernel(const float* __restrict__ h, int n, const float* __restrict__ w,
                                const float* __restrict__ b, float* __restrict__ probs,
                                int32_t* __restrict__ argmax) {
@@ -281,6 +409,28 @@ hipError_t bilstm_launch(const float* seq, int n, int T, int D, const float* wf,
   dim3 grid(blocks_for(n, LSTM_ROWS), 2);
   hipLaunchKernelGGL(bilstm_kernel<128>, grid, dim3(256), 0, s, seq, n, T, wf, wb, bf, bb, out);
   return hipGetLastError();
+}
+
+hipError_t bilstm_h3_launch(const float* seq, int n, int T, int D, const uint16_t* wfh,
+                            const uint16_t* wfl, const uint16_t* wbh, const uint16_t* wbl,
+                            const float* bf, const float* bb, float* out, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  if (D != 128) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(bilstm_h3_kernel<128>, dim3(blocks_for(n, LSTM_ROWS), 2), dim3(512), 0, s, seq,
+                     n, T, wfh, wfl, wbh, wbl, bf, bb, out);
+  return hipGetLastError();
+}
+
+void bilstm_h3_split_weights(const float* wcat, int D, uint16_t* hi, uint16_t* lo) {
+  const int K = 256 + D;
+  for (int j = 0; j < 1024; ++j)
+    for (int k = 0; k < K; ++k) {
+      const float v = wcat[(size_t)k * 1024 + j];
+      const _Float16 h = (_Float16)v;
+      const _Float16 l = (_Float16)((v - (float)h) * LSTM_LO);
+      memcpy(&hi[(size_t)j * K + k], &h, 2);
+      memcpy(&lo[(size_t)j * K + k], &l, 2);
+    }
 }
 
 hipError_t od_head_launch(const float* h, int n, const float* w, const float* b, float* probs,
