@@ -173,26 +173,36 @@ __global__ void __launch_bounds__(256) bilstm_kernel(const float* __restrict__ s
 
 // ---- 3xFP16 BiLSTM ----------------------------------------------------------------------------
 // The same recurrence with the [32 x 384] x [384 x 1024] step product on the f16 MFMA
-// (v_mfma_f32_32x32x16_f16) as error-compensated 3xFP16 (conv_h3.hip): A = [h_{t-1} | x_t] split
-// into fp16 hi/lo in LDS, B = the stacked kernels pre-split on the host and TRANSPOSED to
-// [1024 gate columns][384 k] so a lane's 8 k-values are one 16-B load.  Eight waves: wave w owns
-// hidden units [32w, 32w + 32) of all four gates (4 accumulator tiles x {hi*hi, hi*lo + lo*hi}), so
-// the gate math and the c-state stay in registers as in the f32 kernel.
+// (v_mfma_f32_32x32x16_f16) with 3xFP16 products: A = [h_{t-1} | x_t] split into fp16 hi/lo in LDS,
+// B = the stacked kernels pre-split on the host and TRANSPOSED to [1024 gate columns][384 k] so a
+// lane's 8 k-values are one 16-B load.  Unlike conv_h3 the lo halves are not rescaled by 2^11, so
+// hi*hi, hi*lo and lo*hi accumulate into ONE f32 accumulator per gate tile (the registers that frees
+// hold the next k-step's B fragments: the weight stream from L2 is what the step waits on); to keep
+// the lo halves out of the fp16 subnormals both operands are scaled by exact powers of two first
+// (weights x 2^8 on the host, [h | x] x 2^6 here) and the accumulator is unscaled once.  Eight waves: wave w
+// owns hidden units [32w, 32w + 32) of all four gates, so the gate math stays in registers; the
+// c-state stays in registers.
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
-constexpr float LSTM_LO = 2048.0f;
 
 // gate nonlinearities on the hardware exp / rcp (a few ulp from expf / tanhf; far inside the 1e-4
-// probability tolerance) -- fewer registers live beside the 128 accumulators
+// probability tolerance)
 MMLA_DEV float sigm_f(float z) { return __frcp_rn(1.0f + __expf(-z)); }
 MMLA_DEV float tanh_f(float x) { return 1.0f - 2.0f * __frcp_rn(1.0f + __expf(2.0f * x)); }
 
-MMLA_DEV void split1(float v, _Float16& h, _Float16& l) {
+constexpr float LSTM_WS = 256.0f;   // weight scale (bilstm_h3_split_weights)
+constexpr float LSTM_AS = 64.0f;    // [h | x] scale
+constexpr float LSTM_UNSCALE = 1.0f / (LSTM_WS * LSTM_AS);
+
+MMLA_DEV void split1(float v, _Float16& h, _Float16& l) {   // v * 2^6 = hi + lo
+  v *= LSTM_AS;
   h = (_Float16)v;
-  l = (_Float16)((v - (float)h) * LSTM_LO);
+  l = (_Float16)(v - (float)h);
 }
 
-template <int D>
+// MT 32-clip row tiles per workgroup (1, or 2 where the batch still fills the chip: half the weight
+// stream per clip); PF: prefetch the next k-step's B fragments (MT 1 only: registers)
+template <int D, int MT>
 __global__ void __launch_bounds__(512) bilstm_h3_kernel(const float* __restrict__ seq, int n, int T,
                                                         const uint16_t* __restrict__ wfh,
                                                         const uint16_t* __restrict__ wfl,
@@ -202,42 +212,42 @@ __global__ void __launch_bounds__(512) bilstm_h3_kernel(const float* __restrict_
                                                         const float* __restrict__ bb,
                                                         float* __restrict__ out) {
   constexpr int K = LSTM_U + D;          // 384
+  constexpr int KST = K / 16;            // k-steps
   constexpr int LDA = K + 8;             // fp16 per A row (16-B pad)
   constexpr int NTH = 512;
-  __shared__ __attribute__((aligned(16))) _Float16 Ahi[LSTM_ROWS * LDA];
-  __shared__ __attribute__((aligned(16))) _Float16 Alo[LSTM_ROWS * LDA];
-  __shared__ float Cs[LSTM_ROWS * LSTM_U];   // c-state (registers are taken by the accumulators)
+  constexpr int ROWS = 32 * MT;
+  constexpr bool PF = MT == 1;
+  __shared__ __attribute__((aligned(16))) _Float16 Ahi[ROWS * LDA];
+  __shared__ __attribute__((aligned(16))) _Float16 Alo[ROWS * LDA];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int dir = blockIdx.y;
   const uint16_t* __restrict__ Wh = dir == 0 ? wfh : wbh;
   const uint16_t* __restrict__ Wl = dir == 0 ? wfl : wbl;
   const float* __restrict__ B = dir == 0 ? bf : bb;
-  const int64_t c0 = (int64_t)blockIdx.x * LSTM_ROWS;
+  const int64_t c0 = (int64_t)blockIdx.x * ROWS;
 
-  for (int e = tid; e < LSTM_ROWS * LSTM_U; e += NTH) {   // h_{-1} = 0
+  for (int e = tid; e < ROWS * LSTM_U; e += NTH) {   // h_{-1} = 0
     Ahi[(e / LSTM_U) * LDA + e % LSTM_U] = (_Float16)0.0f;
     Alo[(e / LSTM_U) * LDA + e % LSTM_U] = (_Float16)0.0f;
   }
   const int col = 32 * wave + (lane & 31);   // hidden unit of this lane's accumulator column
   const int koff = 8 * (lane >> 5);
-  float bias[4];
-#pragma unroll
-  for (int g = 0; g < 4; ++g) bias[g] = B[g * LSTM_U + col];
-  const uint16_t* wh[4];
-  const uint16_t* wl[4];
-#pragma unroll
-  for (int g = 0; g < 4; ++g) {
-    wh[g] = Wh + (size_t)(g * LSTM_U + col) * K + koff;
-    wl[g] = Wl + (size_t)(g * LSTM_U + col) * K + koff;
-  }
+  // gate g's B rows: (g * 256 + col) * K + koff; g advances by 256 * K
+  const uint16_t* wh0 = Wh + (size_t)col * K + koff;
+  const uint16_t* wl0 = Wl + (size_t)col * K + koff;
+  constexpr size_t GS = (size_t)LSTM_U * K;
   const _Float16* arow_h = Ahi + (lane & 31) * LDA + koff;
   const _Float16* arow_l = Alo + (lane & 31) * LDA + koff;
-  for (int e = tid; e < LSTM_ROWS * LSTM_U; e += NTH) Cs[e] = 0.0f;
+  float cst[MT][16];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) cst[mt][r] = 0.0f;
 
   for (int s = 0; s < T; ++s) {
     const int t = dir == 0 ? s : T - 1 - s;
     // x_t -> A[:, 256:256+D] (float4 loads, split once)
-    for (int e = tid; e < LSTM_ROWS * D / 4; e += NTH) {
+    for (int e = tid; e < ROWS * D / 4; e += NTH) {
       const int r = e / (D / 4), d4 = e - r * (D / 4);
       const int64_t clip = c0 + r;
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -251,48 +261,82 @@ __global__ void __launch_bounds__(512) bilstm_h3_kernel(const float* __restrict_
       *reinterpret_cast<f16x4*>(Ahi + r * LDA + LSTM_U + 4 * d4) = hv;
       *reinterpret_cast<f16x4*>(Alo + r * LDA + LSTM_U + 4 * d4) = lv;
     }
-    __syncthreads();
-    f32x16 a1[4], a2[4];
+    f16x8 bh[4], bl[4];
+    if constexpr (PF) {
 #pragma unroll
-    for (int g = 0; g < 4; ++g)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        a1[g][r] = bias[g];
-        a2[g][r] = 0.0f;
+      for (int g = 0; g < 4; ++g) {   // k-step 0's B: issued before the barrier
+        bh[g] = *reinterpret_cast<const f16x8*>(wh0 + g * GS);
+        bl[g] = *reinterpret_cast<const f16x8*>(wl0 + g * GS);
       }
-#pragma unroll 1
-    for (int ks = 0; ks < K / 16; ++ks) {
-      const f16x8 ah = *reinterpret_cast<const f16x8*>(arow_h + 16 * ks);
-      const f16x8 al = *reinterpret_cast<const f16x8*>(arow_l + 16 * ks);
+    }
+    __syncthreads();
+    f32x16 acc[MT][4];
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const f16x8 bh = *reinterpret_cast<const f16x8*>(wh[g] + 16 * ks);
-        const f16x8 bl = *reinterpret_cast<const f16x8*>(wl[g] + 16 * ks);
-        a1[g] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, a1[g], 0, 0, 0);
-        a2[g] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, a2[g], 0, 0, 0);
-        a2[g] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, a2[g], 0, 0, 0);
+    for (int g = 0; g < 4; ++g) {
+      const float bv = B[g * LSTM_U + col] * (LSTM_WS * LSTM_AS);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[mt][g][r] = bv;
+    }
+#pragma unroll 2
+    for (int ks = 0; ks < KST; ++ks) {
+      f16x8 nh[4], nl[4];
+      if constexpr (PF) {   // next k-step's B under this one's MFMAs
+        const int kn = ks + 1 < KST ? ks + 1 : ks;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          nh[g] = *reinterpret_cast<const f16x8*>(wh0 + g * GS + 16 * kn);
+          nl[g] = *reinterpret_cast<const f16x8*>(wl0 + g * GS + 16 * kn);
+        }
+      } else {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          bh[g] = *reinterpret_cast<const f16x8*>(wh0 + g * GS + 16 * ks);
+          bl[g] = *reinterpret_cast<const f16x8*>(wl0 + g * GS + 16 * ks);
+        }
+      }
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const f16x8 ah = *reinterpret_cast<const f16x8*>(arow_h + 32 * mt * LDA + 16 * ks);
+        const f16x8 al = *reinterpret_cast<const f16x8*>(arow_l + 32 * mt * LDA + 16 * ks);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          acc[mt][g] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[g], acc[mt][g], 0, 0, 0);
+          acc[mt][g] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl[g], acc[mt][g], 0, 0, 0);
+          acc[mt][g] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[g], acc[mt][g], 0, 0, 0);
+        }
+      }
+      if constexpr (PF) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          bh[g] = nh[g];
+          bl[g] = nl[g];
+        }
       }
     }
     __syncthreads();   // every wave has read h_{t-1}
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-      const float ig = sigm_f(a1[0][r] + a2[0][r] * (1.0f / LSTM_LO));
-      const float fg = sigm_f(a1[1][r] + a2[1][r] * (1.0f / LSTM_LO));
-      const float gg = tanh_f(a1[2][r] + a2[2][r] * (1.0f / LSTM_LO));
-      const float og = sigm_f(a1[3][r] + a2[3][r] * (1.0f / LSTM_LO));
-      const float c = fg * Cs[row * LSTM_U + col] + ig * gg;
-      Cs[row * LSTM_U + col] = c;
-      const float h = og * tanh_f(c);
-      if (s == T - 1) {   // the last state (Keras return_sequences=False), float32
-        const int64_t clip = c0 + row;
-        if (clip < n) out[clip * 512 + dir * LSTM_U + col] = h;
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = 32 * mt + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        const float ig = sigm_f(acc[mt][0][r] * LSTM_UNSCALE);
+        const float fg = sigm_f(acc[mt][1][r] * LSTM_UNSCALE);
+        const float gg = tanh_f(acc[mt][2][r] * LSTM_UNSCALE);
+        const float og = sigm_f(acc[mt][3][r] * LSTM_UNSCALE);
+        const float c = fg * cst[mt][r] + ig * gg;
+        cst[mt][r] = c;
+        const float h = og * tanh_f(c);
+        if (s == T - 1) {   // the last state (Keras return_sequences=False), float32
+          const int64_t clip = c0 + row;
+          if (clip < n) out[clip * 512 + dir * LSTM_U + col] = h;
+        }
+        _Float16 hh, hl;
+        split1(h, hh, hl);
+        Ahi[row * LDA + col] = hh;
+        Alo[row * LDA + col] = hl;
       }
-      _Float16 hh, hl;
-      split1(h, hh, hl);
-      Ahi[row * LDA + col] = hh;
-      Alo[row * LDA + col] = hl;
-    }
   }
 }
 
@@ -416,8 +460,10 @@ hipError_t bilstm_h3_launch(const float* seq, int n, int T, int D, const uint16_
                             const float* bf, const float* bb, float* out, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   if (D != 128) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(bilstm_h3_kernel<128>, dim3(blocks_for(n, LSTM_ROWS), 2), dim3(512), 0, s, seq,
-                     n, T, wfh, wfl, wbh, wbl, bf, bb, out);
+  // (MT 2 -- 64 clips per workgroup, half the weight stream per clip -- needs ~290 registers per
+  // lane: spills at two waves per SIMD, so one 32-clip tile)
+  hipLaunchKernelGGL((bilstm_h3_kernel<128, 1>), dim3(blocks_for(n, LSTM_ROWS), 2), dim3(512), 0, s,
+                     seq, n, T, wfh, wfl, wbh, wbl, bf, bb, out);
   return hipGetLastError();
 }
 
@@ -425,9 +471,9 @@ void bilstm_h3_split_weights(const float* wcat, int D, uint16_t* hi, uint16_t* l
   const int K = 256 + D;
   for (int j = 0; j < 1024; ++j)
     for (int k = 0; k < K; ++k) {
-      const float v = wcat[(size_t)k * 1024 + j];
+      const float v = wcat[(size_t)k * 1024 + j] * LSTM_WS;   // exact power-of-two scale
       const _Float16 h = (_Float16)v;
-      const _Float16 l = (_Float16)((v - (float)h) * LSTM_LO);
+      const _Float16 l = (_Float16)(v - (float)h);   // not rescaled (bilstm_h3_kernel)
       memcpy(&hi[(size_t)j * K + k], &h, 2);
       memcpy(&lo[(size_t)j * K + k], &l, 2);
     }

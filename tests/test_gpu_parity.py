@@ -234,7 +234,7 @@ def test_od_layerwise_trace(ctx):
         assert got.shape == want.shape, (stage, got.shape, want.shape)
         errs[stage] = float(np.abs(got - want).max() / (np.abs(want).max() + 1e-12))
     print('relative max-abs error per stage:', errs)
-    assert all(e < 1e-5 for e in errs.values()), errs
+    assert all(e < 1e-5 for e in errs.values()), str(errs)
 
 
 @pytest.mark.parametrize('prec', [0, 1])
