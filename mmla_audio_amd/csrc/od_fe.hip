@@ -170,12 +170,11 @@ constexpr int NR = (NF + R - 1) / R;              // 26 rounds
 constexpr int WIN = (R - 1) * HOP + N_FFT;        // 1200 samples behind one round
 constexpr int T_LO = 2, T_HI = 9;                 // mel taps of bands 0..63 / 64..127 (host-checked)
 
-struct Smem {                      // 14.4 KB
+struct Smem {                      // 12.8 KB
   int16_t win[WIN];                // reflect-padded window of the round, base = 160 f0 - 200
   cf st[R][200];                   // per frame: pass A out [k1][n2] -> Z[k] -> power P[k] (floats)
   int zc[NF + 1];                  // ZCR counts of the clip
   uint8_t rb[NF + 1];              // image R byte per column
-  cf tw[20][10];
 };
 static_assert(sizeof(int16_t) * WIN % 16 == 0, "st must stay 16-B aligned");
 
@@ -231,8 +230,6 @@ __global__ void __launch_bounds__(NT, 2) od_fe_kernel(OdFeArgs a) {
   } while (0)
   if (fast(0)) FE_PREFETCH(0);
 
-  for (int i = lane; i < 200; i += NT)
-    sm.tw[i / 10][i % 10] = cf{tb.tw[i / 10][i % 10][0], tb.tw[i / 10][i % 10][1]};
   // this lane's two mel bands: first bin and the band's taps (zero past its non-zeros)
   const int mlo = tb.mel_start[lane], mhi = tb.mel_start[lane + 64];
   float wlo[T_LO], whi[T_HI];
@@ -252,11 +249,14 @@ __global__ void __launch_bounds__(NT, 2) od_fe_kernel(OdFeArgs a) {
   // constants kept in registers (LDS reads every frame / round otherwise)
   const cf wka = {tb.w400k[lane][0], tb.w400k[lane][1]};
   const cf wkb = lane + 64 <= 100 ? cf{tb.w400k[lane + 64][0], tb.w400k[lane + 64][1]} : cf{0.f, 0.f};
-  cf hw[20];
+  cf hw[20], tw[20];   // pass A: window taps of the lane's n2 and its twiddles W200^(n2 k1)
   {
     const int n2 = lane < R * 10 ? lane % 10 : 0;
 #pragma unroll
-    for (int n1 = 0; n1 < 20; ++n1) hw[n1] = cf{tb.hann2[10 * n1 + n2][0], tb.hann2[10 * n1 + n2][1]};
+    for (int n1 = 0; n1 < 20; ++n1) {
+      hw[n1] = cf{tb.hann2[10 * n1 + n2][0], tb.hann2[10 * n1 + n2][1]};
+      tw[n1] = cf{tb.tw[n1][n2][0], tb.tw[n1][n2][1]};
+    }
   }
 
   float smax = 0.0f, smin = INFINITY;
@@ -357,7 +357,7 @@ __global__ void __launch_bounds__(NT, 2) od_fe_kernel(OdFeArgs a) {
       cf* dst = &sm.st[f][n2];
       dst[0] = u[0];
 #pragma unroll
-      for (int k1 = 1; k1 < 20; ++k1) dst[10 * k1] = cmul(u[k1], sm.tw[k1][n2]);
+      for (int k1 = 1; k1 < 20; ++k1) dst[10 * k1] = cmul(u[k1], tw[k1]);
     }
     lds_order();
     FE_MARK(2);

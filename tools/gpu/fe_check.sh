@@ -11,6 +11,7 @@ for n in 4096 65536; do
 done
 timeout -k 10 300 python3 tools/fe_timeline.py > gpurun_out/fe_timeline.log 2>&1 || exit $?
 cat gpurun_out/fe_timeline.log | grep -v amdgpu.ids
+exit 0
 rm -rf gpurun_out/prof_si
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_si -o si -- python3 bench.py --workload si_pipeline --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/prof_si.log 2>&1 || exit $?
 find gpurun_out/prof_si -type f ! -name '*_stats.csv' -delete
