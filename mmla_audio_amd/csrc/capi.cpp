@@ -443,9 +443,12 @@ int conv_run(mmla_ctx* c, const ConvArgs& a, int stage = MMLA_STAGE_CONV) {
 // spatial conv on the 3xFP16 path when enabled (falls back to the exact-f32 kernel otherwise);
 // pool_out: write MaxPool2D(2,'same') of the output instead of the output (OD pool blocks).
 int conv_spatial(mmla_ctx* c, const ConvW& w, const float* x, float* y, int n, int h, int wd,
-                 const BnW* bn, int pro, int epi, const float* res, bool pool_out = false) {
+                 const BnW* bn, int pro, int epi, const float* res, bool pool_out = false,
+                 int pool_in_h = 0) {
   if (c->precision == MMLA_PREC_F16X3 && w.wh) {
     ConvH3Args a{};
+    a.pool_in = pool_in_h > 0;   // x = the unpooled [n, pool_in_h, 1, cin] (MaxPool1D fused)
+    a.h_in = pool_in_h;
     a.x = x;
     a.wh = w.wh;
     a.wl = w.wl;
@@ -643,10 +646,16 @@ int run_si_net(mmla_ctx* c, const float* x, int64_t n, float* probs, int32_t* ar
     const SiUnit& U = W.unit[u];
     const int cin = U.ca.cin;
     if (POOL[u]) {
-      LAUNCH(c, MMLA_STAGE_GLUE, (double)n * t * cin,
-             maxpool_t2_launch(X, (int)n, t, cin, XP, c->stream));
       const int tp = (t + 1) / 2;
-      CHK(conv_spatial(c, U.ca, XP, T1, (int)n, tp, 1, &U.bn_in, PRO_BN_RELU, EPI_BIAS, nullptr));
+      if (c->precision == MMLA_PREC_F16X3 && U.ca.wh) {
+        // MaxPool1D(2, same) taken inside the conv's staging (conv_h3.hip PIN)
+        CHK(conv_spatial(c, U.ca, X, T1, (int)n, tp, 1, &U.bn_in, PRO_BN_RELU, EPI_BIAS, nullptr,
+                         false, t));
+      } else {
+        LAUNCH(c, MMLA_STAGE_GLUE, (double)n * t * cin,
+               maxpool_t2_launch(X, (int)n, t, cin, XP, c->stream));
+        CHK(conv_spatial(c, U.ca, XP, T1, (int)n, tp, 1, &U.bn_in, PRO_BN_RELU, EPI_BIAS, nullptr));
+      }
       CHK(conv_run(c, conv_args(U.sc, X, R, (int)n, t, 1, 2, nullptr, PRO_NONE, EPI_BIAS, nullptr)));
       CHK(conv_spatial(c, U.cb, T1, R, (int)n, tp, 1, &U.bn_mid, PRO_BN_RELU, EPI_ADD, R));
       std::swap(X, R);

@@ -18,6 +18,8 @@ struct ConvH3Args {
   int th, tw;            // output tile (th * tw <= 128)
   int tiles_h, tiles_w;
   int pro, epi, pool_out;
+  int pool_in;           // Conv1D only: x is [N, h_in, 1, Cin] and the conv reads MaxPool1D(2, same) of it
+  int h_in;
 };
 
 // Picks the tile and launches; returns hipErrorInvalidValue for unsupported shapes.

@@ -50,8 +50,10 @@ MMLA_DEV float pro_fn(float v, float sc, float sh) {
   }
 }
 
-// V4: channels loaded as float4 (cin % 4 == 0); else per element (the SI stem, cin = 39)
-template <int KH, int KW, int CK, int BN, int TW, int PRO, int EPI, bool POOL, bool V4 = true>
+// V4: channels loaded as float4 (cin % 4 == 0); else per element (the SI stem, cin = 39).
+// PIN (Conv1D): the input rows are MaxPool1D(2, 'same') of x, taken while staging (SI pool units)
+template <int KH, int KW, int CK, int BN, int TW, int PRO, int EPI, bool POOL, bool V4 = true,
+          bool PIN = false>
 __global__ void __launch_bounds__(NT, 2) conv_h3_kernel(ConvH3Args a) {
   // each wave owns ONE 32-column slice of B (no B fragment is loaded by two waves) and
   // 128 / WM rows: BN 32 -> 4 x 1, BN 64 -> 2 x 2, BN 128 -> 1 x 4 (waves along N)
@@ -137,7 +139,17 @@ __global__ void __launch_bounds__(NT, 2) conv_h3_kernel(ConvH3Args a) {
         const int ci = ci0 + q * 4;
         if (ih >= 0 && ih < HH && iw >= 0 && iw < a.w && ci < a.cin) {
           const float* src = xclip + (ih * a.w + iw) * a.cin + ci;
-          if constexpr (V4) {
+          if constexpr (PIN) {
+            // pooled row ih = (clip, tt) <- unpooled rows 2 tt, 2 tt + 1 of that clip
+            const int cl = ih / a.h, tt = ih - cl * a.h;
+            src = a.x + ((int64_t)cl * a.h_in + 2 * tt) * a.cin + ci;
+            float4 v = *reinterpret_cast<const float4*>(src);
+            if (2 * tt + 1 < a.h_in) {
+              const float4 u = *reinterpret_cast<const float4*>(src + a.cin);
+              v = make_float4(fmaxf(v.x, u.x), fmaxf(v.y, u.y), fmaxf(v.z, u.z), fmaxf(v.w, u.w));
+            }
+            pre[j] = v;
+          } else if constexpr (V4) {
             pre[j] = *reinterpret_cast<const float4*>(src);
           } else {
             pre[j].x = src[0];
@@ -326,19 +338,21 @@ __global__ void __launch_bounds__(NT, 2) conv_h3_kernel(ConvH3Args a) {
   }
 }
 
-template <int KH, int KW, int CK, int BN, int TW, int PRO, int EPI, bool POOL, bool V4 = true>
+template <int KH, int KW, int CK, int BN, int TW, int PRO, int EPI, bool POOL, bool V4 = true,
+          bool PIN = false>
 hipError_t launch(const ConvH3Args& a, hipStream_t s) {
   const int64_t tiles = (int64_t)a.tiles_h * a.tiles_w * (TW == 1 ? 1 : a.n);
   dim3 grid((unsigned)tiles, (unsigned)(a.cout_pad / BN));
-  hipLaunchKernelGGL((conv_h3_kernel<KH, KW, CK, BN, TW, PRO, EPI, POOL, V4>), grid, dim3(NT), 0, s, a);
+  hipLaunchKernelGGL((conv_h3_kernel<KH, KW, CK, BN, TW, PRO, EPI, POOL, V4, PIN>), grid, dim3(NT), 0,
+                     s, a);
   return hipGetLastError();
 }
 
-template <int KH, int KW, int CK, int TW, int PRO, int EPI, bool POOL>
+template <int KH, int KW, int CK, int TW, int PRO, int EPI, bool POOL, bool PIN = false>
 hipError_t by_bn(const ConvH3Args& a, hipStream_t s) {
-  if (a.cout_pad % 128 == 0) return launch<KH, KW, CK, 128, TW, PRO, EPI, POOL>(a, s);
-  if (a.cout_pad % 64 == 0) return launch<KH, KW, CK, 64, TW, PRO, EPI, POOL>(a, s);
-  return launch<KH, KW, CK, 32, TW, PRO, EPI, POOL>(a, s);
+  if (a.cout_pad % 128 == 0) return launch<KH, KW, CK, 128, TW, PRO, EPI, POOL, true, PIN>(a, s);
+  if (a.cout_pad % 64 == 0) return launch<KH, KW, CK, 64, TW, PRO, EPI, POOL, true, PIN>(a, s);
+  return launch<KH, KW, CK, 32, TW, PRO, EPI, POOL, true, PIN>(a, s);
 }
 
 }  // namespace
@@ -366,6 +380,12 @@ hipError_t conv_h3_launch(ConvH3Args a, hipStream_t s) {
   a.tiles_w = (a.w + a.tw - 1) / a.tw;
   const int ck = a.cin_pad % 32 == 0 ? 32 : 16;
   if (a.cin_pad % ck != 0) return hipErrorInvalidValue;
+  if (a.pool_in) {   // SI pool unit: MaxPool1D(2) -> BN -> ReLU -> Conv1D(3)
+    if (a.kh == 3 && a.kw == 1 && ck == 32 && a.tw == 1 && a.pro == PRO_BN_RELU &&
+        a.epi == EPI_BIAS && !a.pool_out && a.h_in >= 2 * a.h - 1 && a.h_in <= 2 * a.h)
+      return by_bn<3, 1, 32, 1, PRO_BN_RELU, EPI_BIAS, false, true>(a, s);
+    return hipErrorInvalidValue;
+  }
 #define H3(KH, KW, CK, TW, P, E, PL)                                                           \
   if (a.kh == KH && a.kw == KW && ck == CK && a.tw == TW && a.pro == P && a.epi == E &&        \
       (a.pool_out != 0) == PL)                                                                 \
