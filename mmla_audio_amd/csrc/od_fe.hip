@@ -170,9 +170,11 @@ constexpr int NR = (NF + R - 1) / R;              // 26 rounds
 constexpr int WIN = (R - 1) * HOP + N_FFT;        // 1200 samples behind one round
 constexpr int T_LO = 2, T_HI = 9;                 // mel taps of bands 0..63 / 64..127 (host-checked)
 
-struct Smem {                      // 12.8 KB
+constexpr int P2W = 212;           // power-row pitch (>= 201 + the widest band's taps: zero pad)
+struct Smem {                      // 18.0 KB
   int16_t win[WIN];                // reflect-padded window of the round, base = 160 f0 - 200
-  cf st[R][200];                   // per frame: pass A out [k1][n2] -> Z[k] -> power P[k] (floats)
+  cf st[R][200];                   // per frame: pass A out [k1][n2] -> Z[k]
+  float2 p2[R / 2][P2W];           // power spectra of frame pairs, interleaved: P[2q + c][k] = p2[q][k].c
   int zc[NF + 1];                  // ZCR counts of the clip
   uint8_t rb[NF + 1];              // image R byte per column
 };
@@ -258,6 +260,10 @@ __global__ void __launch_bounds__(NT, 2) od_fe_kernel(OdFeArgs a) {
       tw[n1] = cf{tb.tw[n1][n2][0], tb.tw[n1][n2][1]};
     }
   }
+
+  for (int i = lane; i < (R / 2) * (P2W - 201); i += NT)   // power-row pads read by the last taps
+    sm.p2[i / (P2W - 201)][201 + i % (P2W - 201)] = float2{0.0f, 0.0f};
+  static_assert(R % 2 == 0, "frame pairs");
 
   float smax = 0.0f, smin = INFINITY;
   for (int r = 0; r < NR; ++r) {
@@ -384,11 +390,11 @@ __global__ void __launch_bounds__(NT, 2) od_fe_kernel(OdFeArgs a) {
       lds_order();
     }
     FE_MARK(3);
-    // ---- split: power spectrum P[f][0..200] over the frame's own Z (all reads before writes) ------
+    // ---- split: power spectrum P[f][0..200] into the frame pair's interleaved row -----------------
 #pragma unroll
     for (int f = 0; f < R; ++f) {
       const cf* Z = sm.st[f];
-      float* P = reinterpret_cast<float*>(sm.st[f]);
+      float* P = reinterpret_cast<float*>(sm.p2[f >> 1]) + (f & 1);   // P[k] at P[2 k]
       const int ka = lane, kb = lane + 64;
       const bool hb = kb <= 100;
       const cf za = Z[ka], zar = Z[ka == 0 ? 0 : 200 - ka], wa = wka;
@@ -401,41 +407,53 @@ __global__ void __launch_bounds__(NT, 2) od_fe_kernel(OdFeArgs a) {
       lds_order();
       float p0, p1;
       split_power(za, zar, wa, p0, p1);
-      P[ka] = p0;
-      P[200 - ka] = p1;
+      P[2 * ka] = p0;
+      P[2 * (200 - ka)] = p1;
       if (hb) {
         split_power(zb, zbr, wb, p0, p1);
-        P[kb] = p0;
-        P[200 - kb] = p1;
+        P[2 * kb] = p0;
+        P[2 * (200 - kb)] = p1;
       }
-      lds_order();
     }
+    lds_order();
     FE_MARK(4);
     // ---- mel: S[m][f] = sum_j w[m][j] P[f][start_m + j] -> 10 log10 S to the frame-major scratch ---
-    // (taps past a band's non-zeros are exact zeros times finite LDS words: same sum)
-    // every round issues the same 12 stores (frames past the clip, last round only, repeat the
-    // round's first frame): the compiler can then count them in the next round's window wait
+    // two frames per packed FMA (the pair's interleaved power row); taps past a band's non-zeros
+    // are exact zeros times finite LDS words (the row pad is zeroed): same sum.  Every round issues
+    // the same 12 stores (frames past the clip, last round only, repeat the round's first frame):
+    // the compiler can then count them in the next round's window wait
     float s0 = 0.0f, s1 = 0.0f;
 #pragma unroll
-    for (int f = 0; f < R; ++f) {
-      const float* P = reinterpret_cast<const float*>(sm.st[f]);
-      float a0 = 0.0f, a1 = 0.0f;
+    for (int q = 0; q < R / 2; ++q) {
+      const float2* P = sm.p2[q];
+      float2 a0 = {0.0f, 0.0f}, a1 = {0.0f, 0.0f};
 #pragma unroll
-      for (int j = 0; j < T_LO; ++j) a0 = fmaf(wlo[j], P[mlo + j], a0);
-#pragma unroll
-      for (int j = 0; j < T_HI; ++j) a1 = fmaf(whi[j], P[mhi + j], a1);
-      if (f == 0) {
-        s0 = a0;
-        s1 = a1;
-      } else if (f0 + f >= NF) {
-        a0 = s0;
-        a1 = s1;
+      for (int j = 0; j < T_LO; ++j) {
+        const float2 v = P[mlo + j];
+        a0 = float2{fmaf(wlo[j], v.x, a0.x), fmaf(wlo[j], v.y, a0.y)};
       }
-      float* row = scr + min(f0 + f, NF - 1) * NMEL;
-      row[lane] = db10(a0);
-      row[lane + 64] = db10(a1);
-      smax = fmaxf(smax, fmaxf(a0, a1));
-      smin = fminf(smin, fminf(a0, a1));
+#pragma unroll
+      for (int j = 0; j < T_HI; ++j) {
+        const float2 v = P[mhi + j];
+        a1 = float2{fmaf(whi[j], v.x, a1.x), fmaf(whi[j], v.y, a1.y)};
+      }
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int f = 2 * q + c;
+        float b0 = c ? a0.y : a0.x, b1 = c ? a1.y : a1.x;
+        if (f == 0) {
+          s0 = b0;
+          s1 = b1;
+        } else if (f0 + f >= NF) {
+          b0 = s0;
+          b1 = s1;
+        }
+        float* row = scr + min(f0 + f, NF - 1) * NMEL;
+        row[lane] = db10(b0);
+        row[lane + 64] = db10(b1);
+        smax = fmaxf(smax, fmaxf(b0, b1));
+        smin = fminf(smin, fminf(b0, b1));
+      }
     }
     FE_MARK(5);
   }
@@ -871,7 +889,10 @@ extern "C" int mmla_debug_fe_times(unsigned long long* host) {
 size_t od_fe_smem_bytes() { return fe_impl() == 1 ? sizeof(v1::Smem) : sizeof(v2::Smem); }
 
 bool od_fe_tables_ok(const OdFeTables& t) {
-  return t.mel_taps_lo <= v2::T_LO && t.mel_taps_hi <= v2::T_HI;
+  if (t.mel_taps_lo > v2::T_LO || t.mel_taps_hi > v2::T_HI) return false;
+  for (int m = 0; m < 128; ++m)   // the last tap of every band stays inside the zero-padded row
+    if (t.mel_start[m] + (m < 64 ? v2::T_LO : v2::T_HI) > v2::P2W) return false;
+  return true;
 }
 
 static void launch_v2(const OdFeArgs& a, int64_t n, hipStream_t s) {
