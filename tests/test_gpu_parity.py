@@ -189,6 +189,37 @@ def test_device_pointer_mode_matches_host(ctx):
     assert np.array_equal(d_a.cpu().numpy(), ah)
 
 
+@pytest.mark.parametrize('offset,stride', [(1, 40001), (3, 40003), (8, 40008)])
+def test_front_ends_misaligned_device_pcm(ctx, offset, stride):
+    """Device-pointer PCM at odd sample offsets / strides: the front-ends' vector window loads need
+    16-B alignment, so these take the scalar window paths -- results must equal the aligned run."""
+    import torch
+    n = 5
+    pcm = synth.batch(720, n, 40000)
+    buf = np.zeros(offset + n * stride, np.int16)
+    for i in range(n):
+        buf[offset + i * stride: offset + i * stride + 40000] = pcm[i]
+    d = torch.from_numpy(buf).cuda()
+    base = d.data_ptr() + 2 * offset
+    norm = torch.empty((n, 128, 151), dtype=torch.float32, device='cuda')
+    zcr = torch.empty((n, 151), dtype=torch.float32, device='cuda')
+    feat = torch.empty((n, 256, 39), dtype=torch.float32, device='cuda')
+    torch.cuda.synchronize()
+    ctx.od_features_dev(base, n, stride, 40000, norm=norm.data_ptr(), zcr=zcr.data_ptr())
+    ctx.si_features_dev(base, n, stride, 40000, feat.data_ptr())
+    ctx.synchronize()
+    f = ctx.od_features(pcm)
+    nn, fa = norm.cpu().numpy(), f['norm']
+    assert np.array_equal(np.isnan(nn), np.isnan(fa))
+    assert np.array_equal(nn[~np.isnan(nn)], fa[~np.isnan(fa)])
+    assert np.array_equal(zcr.cpu().numpy(), f['zcr'])
+    sf, _ = ctx.si_features(pcm)
+    assert np.abs(feat.cpu().numpy() - sf).max() <= 1e-6
+    for i in range(2):
+        ref = si_fe.input_feature_gen(pcm[i])[0]
+        assert np.abs(feat.cpu().numpy()[i] - ref).max() <= 1e-4
+
+
 def test_no_weights_raises(ctx):
     from mmla_audio_amd import _lib
     fresh = _lib.Context(0)
