@@ -146,19 +146,36 @@ int mmla_si_pipeline(mmla_ctx* ctx, const int16_t* pcm, int64_t n_clips, int64_t
                      uint8_t* silent, uint32_t flags);
 
 /*
+ * Stationary spectral-gate noise reduction, replaces nr.reduce_noise(y_noise=noise, y=y, sr=sr,
+ * stationary=True) (OverlapDetection/scripts/record_on_pc.py:208-212,
+ * SpeakerIdentification/scripts/record_on_pc.py:189, speaker_identification_post_processing.py:171)
+ * with noisereduce 2.0.x defaults (n_fft 1024, hop 256, n_std 1.5, 500 Hz x 50 ms mask smoothing,
+ * chunk_size 600000, padding 30000).  sr must be 16000.
+ * mmla_nr_set_noise: noise [n_noise] f32 (librosa.load output; the first chunk_size samples are
+ * used) -> per-bin threshold kept in the context.
+ * mmla_nr_reduce: y [n_signals, stride] f32, each signal `len` samples -> out [n_signals, len] f32;
+ * signals longer than chunk_size are gated chunk by chunk with `padding` samples of context.
+ */
+int mmla_nr_set_noise(mmla_ctx* ctx, const float* noise, int64_t n_noise, int32_t sr,
+                      uint32_t flags);
+int mmla_nr_reduce(mmla_ctx* ctx, const float* y, int64_t n_signals, int64_t stride, int64_t len,
+                   float* out, uint32_t flags);
+
+/*
  * Kernel tracing (replaces the reference's time.time() prints, overlap_detector_run.py:49-104).
  * When enabled, every kernel launch is bracketed by hipEvents on the context stream and its device
  * time is accumulated per stage together with the stage's algorithmic work (bytes for the
  * front-ends, FLOPs for the networks).  mmla_profile_read waits for the recorded events.
  */
-#define MMLA_NSTAGES 6
+#define MMLA_NSTAGES 7
 enum mmla_stage {
   MMLA_STAGE_OD_FE = 0, /* work = algorithmic HBM bytes */
   MMLA_STAGE_SI_FE = 1, /* work = algorithmic HBM bytes */
   MMLA_STAGE_CONV = 2,  /* work = FLOPs (2 * MACs, unpadded) */
   MMLA_STAGE_LSTM = 3,  /* work = FLOPs */
   MMLA_STAGE_GLUE = 4,  /* stem, pooling, mean: work = FLOPs */
-  MMLA_STAGE_HEAD = 5   /* dense + softmax / sigmoid: work = FLOPs */
+  MMLA_STAGE_HEAD = 5,  /* dense + softmax / sigmoid: work = FLOPs */
+  MMLA_STAGE_NR = 6     /* noise gate: work = algorithmic HBM bytes (signal in + out) */
 };
 int mmla_profile_enable(mmla_ctx* ctx, int on);
 

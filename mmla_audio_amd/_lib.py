@@ -32,6 +32,8 @@ _U32 = ctypes.c_uint32
 
 # name -> argtypes (all return int)
 SIGNATURES = {
+    'mmla_nr_set_noise': [_P, _P, _I64, ctypes.c_int32, ctypes.c_uint32],
+    'mmla_nr_reduce': [_P, _P, _I64, _I64, _I64, _P, ctypes.c_uint32],
     'mmla_abi_version': [],
     'mmla_create': [ctypes.c_int, ctypes.POINTER(_P)],
     'mmla_destroy': [_P],
@@ -53,8 +55,8 @@ SIGNATURES = {
     'mmla_debug_od_trace': [_P, _P, _I64, ctypes.c_int, _P, _I64],
 }
 
-NSTAGES = 6
-STAGES = ('od_fe', 'si_fe', 'conv', 'lstm', 'glue', 'head')
+NSTAGES = 7
+STAGES = ('od_fe', 'si_fe', 'conv', 'lstm', 'glue', 'head', 'nr')
 
 _lib = None
 _lock = threading.Lock()
@@ -182,6 +184,28 @@ class Context:
             self.od_classes = int(n_classes)
         else:
             self.si_classes = int(n_classes)
+
+    # -- noise gate --------------------------------------------------------
+    def nr_set_noise(self, noise, sr=16000):
+        """Noise profile for reduce_noise(y_noise=noise, stationary=True): float32 samples."""
+        a = np.ascontiguousarray(noise, dtype=np.float32).ravel()
+        self._check(self.lib.mmla_nr_set_noise(self.h, _ptr(a), a.size, int(sr), 0),
+                    'mmla_nr_set_noise')
+
+    def nr_reduce(self, y):
+        """Gate float32 signals y [n, len] (or [len]) with the current noise profile."""
+        a = np.ascontiguousarray(y, dtype=np.float32)
+        flat = a.ndim == 1
+        if flat:
+            a = a[None]
+        out = np.empty_like(a)
+        self._check(self.lib.mmla_nr_reduce(self.h, _ptr(a), a.shape[0], a.shape[1], a.shape[1],
+                                            _ptr(out), 0), 'mmla_nr_reduce')
+        return out[0] if flat else out
+
+    def nr_reduce_dev(self, y, n, stride, length, out):
+        self._check(self.lib.mmla_nr_reduce(self.h, y, n, stride, length, out, MMLA_DEVICE_PTR),
+                    'mmla_nr_reduce(dev)')
 
     # -- host-array API -----------------------------------------------------------------------
     @staticmethod

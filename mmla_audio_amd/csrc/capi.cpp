@@ -16,6 +16,7 @@
 #include "resblk.h"
 #include "od_fe.h"
 #include "si_fe.h"
+#include "nr.h"
 
 namespace {
 
@@ -102,6 +103,9 @@ struct mmla_ctx {
   std::vector<size_t> ws_size;
   int64_t od_mb = kOdMicrobatch, si_mb = kSiMicrobatch;
   int precision = MMLA_PREC_F16X3;
+  NrTables* nr_tables = nullptr;   // noise gate (nr.hip): tables + the noise profile's threshold
+  float* nr_thresh = nullptr;
+  bool nr_ready = false;
 };
 
 namespace {
@@ -205,7 +209,8 @@ int ws_get(mmla_ctx* c, int slot, size_t bytes, void** out) {
 
 enum Slot {
   S_PCM = 0, S_LENS, S_IMG, S_X, S_T1, S_T2, S_T3, S_SEQ, S_HOUT, S_LOGIT, S_FEAT, S_SILENT,
-  S_OUT0, S_OUT1, S_OUT2, S_OUT3, S_IN, S_FESCR
+  S_OUT0, S_OUT1, S_OUT2, S_OUT3, S_IN, S_FESCR,
+  S_NR_S, S_NR_BITS, S_NR_FMAX, S_NR_FRAMES, S_NR_ITEMS, S_NR_Y
 };
 
 // ---- weights -------------------------------------------------------------------------------------
@@ -757,11 +762,128 @@ int mmla_destroy(mmla_ctx* c) {
     if (p) (void)hipFree(p);
   if (c->od_tables) (void)hipFree(c->od_tables);
   if (c->si_tables) (void)hipFree(c->si_tables);
+  if (c->nr_tables) (void)hipFree(c->nr_tables);
+  if (c->nr_thresh) (void)hipFree(c->nr_thresh);
   (void)prof_collect(c);
   for (hipEvent_t e : c->prof_pool) (void)hipEventDestroy(e);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   delete c;
   return MMLA_OK;
+}
+
+// ---- stationary noise gate ----------------------------------------------------
+
+namespace {
+constexpr int64_t kNrChunk = 600000, kNrPadding = 30000;   // noisereduce 2.0 defaults
+constexpr int64_t kNrItemsPerLaunch = 512;                  // ~3.4 GB of scratch per launch (2.5 s)
+}  // namespace
+
+int mmla_nr_set_noise(mmla_ctx* c, const float* noise, int64_t n_noise, int32_t sr, uint32_t flags) {
+  if (!c) return MMLA_E_INVALID;
+  if (!noise || n_noise < 2) return fail(c, MMLA_E_INVALID, "noise clip needs >= 2 samples");
+  if (sr != 16000) return fail(c, MMLA_E_INVALID, "noise gate supports sr = 16000 (got %d)", sr);
+  HIPCHK(c, hipSetDevice(c->device));
+  const bool dev = flags & MMLA_DEVICE_PTR;
+  if (!c->nr_tables) {
+    NrTables t;
+    nr_build_tables(&t, sr);
+    if (t.ngf != NR_NGF || t.ngt != NR_NGT) return fail(c, MMLA_E_INVALID, "smoothing filter shape");
+    HIPCHK(c, hipMalloc(&c->nr_tables, sizeof(NrTables)));
+    HIPCHK(c, hipMalloc(&c->nr_thresh, (NR_NFFT / 2 + 1) * sizeof(float)));
+    HIPCHK(c, hipMemcpy(c->nr_tables, &t, sizeof(t), hipMemcpyHostToDevice));
+  }
+  const int64_t m = std::min(n_noise, kNrChunk);   // clip_noise_stationary: y_noise[:chunk_size]
+  const int64_t Tn = 1 + m / NR_HOP;
+  const float* dn = noise;
+  void *pdb = nullptr, *pmx = nullptr;
+  if (!dev) {
+    void* p = nullptr;
+    CHK(ws_get(c, S_IN, m * sizeof(float), &p));
+    HIPCHK(c, hipMemcpyAsync(p, noise, m * sizeof(float), hipMemcpyHostToDevice, c->stream));
+    dn = static_cast<const float*>(p);
+  }
+  CHK(ws_get(c, S_NR_FRAMES, (size_t)Tn * (NR_NFFT / 2 + 1) * sizeof(float), &pdb));
+  CHK(ws_get(c, S_NR_FMAX, (size_t)Tn * sizeof(float), &pmx));
+  LAUNCH(c, MMLA_STAGE_NR, (double)m * 4,
+         nr_noise_launch(dn, m, c->nr_tables, static_cast<float*>(pdb), static_cast<float*>(pmx),
+                         1.5f, c->nr_thresh, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->nr_ready = true;
+  return MMLA_OK;
+}
+
+int mmla_nr_reduce(mmla_ctx* c, const float* y, int64_t n_signals, int64_t stride, int64_t len,
+                   float* out, uint32_t flags) {
+  if (!c) return MMLA_E_INVALID;
+  if (n_signals < 0 || len < 0 || (n_signals > 0 && (!y || !out)) ||
+      (n_signals > 1 && stride < len))
+    return fail(c, MMLA_E_INVALID, "bad nr_reduce args");
+  if (!c->nr_ready) return fail(c, MMLA_E_INVALID, "mmla_nr_set_noise must be called first");
+  if (n_signals == 0 || len == 0) return MMLA_OK;
+  HIPCHK(c, hipSetDevice(c->device));
+  const bool dev = flags & MMLA_DEVICE_PTR;
+  // SpectralGate.get_traces: one chunk of `len` when len <= chunk_size, else chunk_size pieces
+  const int64_t keep = len <= kNrChunk ? len : kNrChunk;
+  const int64_t per = (len + keep - 1) / keep;
+  const int64_t L = keep + 2 * kNrPadding;
+  const int T = (int)(1 + L / NR_HOP);
+  const int64_t bins = NR_NFFT / 2 + 1;
+  const int64_t cap = std::max<int64_t>(1, std::min<int64_t>(kNrItemsPerLaunch, (int64_t)(2e10 / ((double)T * (bins * 17 + NR_NFFT * 8 + 8)))));
+  std::vector<NrItem> items;
+  items.reserve(n_signals * per);
+  for (int64_t sgl = 0; sgl < n_signals; ++sgl)
+    for (int64_t k = 0; k < per; ++k)
+      items.push_back(NrItem{sgl * stride, len, k * keep - kNrPadding, sgl * len + k * keep,
+                             std::min(keep, len - k * keep)});
+  // signals: the caller's device pointer, or one host copy per call
+  const float* dy = y;
+  if (!dev) {
+    void* p = nullptr;
+    const int64_t span = (n_signals - 1) * stride + len;
+    CHK(ws_get(c, S_NR_Y, span * sizeof(float), &p));
+    HIPCHK(c, hipMemcpyAsync(p, y, span * sizeof(float), hipMemcpyHostToDevice, c->stream));
+    dy = static_cast<const float*>(p);
+  }
+  float* dout = out;
+  if (!dev) {
+    void* p = nullptr;
+    CHK(ws_get(c, S_OUT0, (size_t)n_signals * len * sizeof(float), &p));
+    dout = static_cast<float*>(p);
+  }
+  for (size_t i0 = 0; i0 < items.size(); i0 += cap) {
+    const int64_t ni = std::min<int64_t>(cap, (int64_t)items.size() - (int64_t)i0);
+    void *pS, *pB, *pM, *pF, *pI;
+    CHK(ws_get(c, S_NR_S, (size_t)ni * T * bins * sizeof(double2), &pS));
+    CHK(ws_get(c, S_NR_BITS, (size_t)ni * T * bins, &pB));
+    CHK(ws_get(c, S_NR_FMAX, (size_t)ni * T * sizeof(double), &pM));
+    CHK(ws_get(c, S_NR_FRAMES, (size_t)ni * T * NR_NFFT * sizeof(double), &pF));
+    CHK(ws_get(c, S_NR_ITEMS, (size_t)ni * sizeof(NrItem), &pI));
+    HIPCHK(c, hipMemcpyAsync(pI, items.data() + i0, ni * sizeof(NrItem), hipMemcpyHostToDevice,
+                             c->stream));
+    NrArgs a{};
+    a.y = dy;
+    a.items = static_cast<const NrItem*>(pI);
+    a.n_items = ni;
+    a.L = L;
+    a.T = T;
+    a.keep0 = kNrPadding;
+    a.keep_len = keep;
+    a.tables = c->nr_tables;
+    a.thresh = c->nr_thresh;
+    a.prop_decrease = 1.0;
+    a.S = static_cast<double2*>(pS);
+    a.bits = static_cast<uint8_t*>(pB);
+    a.fmax = static_cast<double*>(pM);
+    a.frames = static_cast<double*>(pF);
+    a.out = dout;
+    double bytes = 0;
+    for (int64_t i = 0; i < ni; ++i) bytes += 8.0 * items[i0 + i].out_len;   // f32 in + f32 out
+    LAUNCH(c, MMLA_STAGE_NR, bytes, nr_gate_launch(a, c->stream));
+    // the item table / scratch of this launch must not be overwritten by the next one's upload
+    if (i0 + cap < items.size()) HIPCHK(c, hipStreamSynchronize(c->stream));
+  }
+  CHK(copy_back(c, out, 0, dout, (size_t)n_signals * len, dev));
+  return finish(c, dev);
 }
 
 const char* mmla_last_error(const mmla_ctx* c) { return c ? c->err.c_str() : "null context"; }

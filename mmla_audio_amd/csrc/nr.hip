@@ -1,0 +1,383 @@
+// Stationary spectral-gate noise reduction on gfx950, float64 like the
+// reference's chunk buffers.
+//
+// Replaces nr.reduce_noise(y_noise=noise, y=y, sr=sr, stationary=True)
+//   OverlapDetection/scripts/record_on_pc.py:208-212, SpeakerIdentification/scripts/record_on_pc.py:189,
+//   speaker_identification_post_processing.py:171, record_on_pi.py:112
+// i.e. noisereduce 2.0.x SpectralGateStationary on librosa 0.8 stft/istft (oracle/noisereduce.py).
+//
+// Work unit = one "item": a buffer of L = chunk + 2 * padding samples read from a float32 signal
+// (zeros outside it), exactly the float64 buffer SpectralGate._read_chunk builds.  All items of a
+// launch share L, so an item has T = 1 + L / 256 STFT frames (n_fft 1024, hop 256, centre reflect).
+//   nr_stft_kernel     one wave per (item, frame): 1024-point real DFT as a 512-point complex FFT
+//                      of the even/odd-packed frame (radix 8 x 8 x 8 in LDS) + real split -> S[513]
+//                      (complex128 to HBM), mask bit dB > thresh per bin, the frame's max dB; frames
+//                      whose window only covers zeros skip the FFT (S = 0, dB = 10 log10(1e-40))
+//   nr_gate_kernel     one wave per (item, frame) touching the kept interior: the item's max dB,
+//                      mask rows t-3..t+3 OR'ed with (max - 80 > thresh) (top_db clamp), the
+//                      33 x 7 smoothing filter (separable: freq then time, zero outside the array
+//                      like fftconvolve 'same'), S * mask, inverse real FFT, x window -> the frame
+//                      in the time domain (HBM scratch)
+//   nr_ola_kernel      overlap-add of the <= 4 frames covering each kept sample, / window
+//                      sum-square, float32 out
+// The noise profile (per-bin threshold) is computed once per noise clip by nr_noise_db_kernel +
+// nr_noise_thresh_kernel in the reference's float32 arithmetic.
+#include "common.h"
+#include "nr.h"
+
+#include <cmath>
+#include <vector>
+
+namespace {
+
+constexpr int NT = 64;
+constexpr int NFFT = NR_NFFT;       // 1024
+constexpr int HOP = NR_HOP;         // 256
+constexpr int NB = NFFT / 2 + 1;    // 513 bins
+constexpr int NG_F = NR_NGF;        // 33 frequency taps
+constexpr int NG_T = NR_NGT;        // 7 time taps
+
+// complex 8-point DFT in registers (W8^(nk)), in/out natural order
+MMLA_DEV void dft8(cd v[8]) {
+  const double r = 0.70710678118654752440;
+  cd a[4], b[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    a[k] = cadd(v[k], v[k + 4]);
+    b[k] = csub(v[k], v[k + 4]);
+  }
+  b[1] = cmul(b[1], cd{r, -r});
+  b[2] = cmul_negi(b[2]);
+  b[3] = cmul(b[3], cd{-r, -r});
+  // two 4-point DFTs
+  auto dft4 = [](cd& x0, cd& x1, cd& x2, cd& x3) {
+    const cd s02 = cadd(x0, x2), d02 = csub(x0, x2), s13 = cadd(x1, x3), d13 = csub(x1, x3);
+    x0 = cadd(s02, s13);
+    x2 = csub(s02, s13);
+    x1 = cadd(d02, cmul_negi(d13));
+    x3 = csub(d02, cmul_negi(d13));
+  };
+  dft4(a[0], a[1], a[2], a[3]);
+  dft4(b[0], b[1], b[2], b[3]);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    v[2 * k] = a[k];
+    v[2 * k + 1] = b[k];
+  }
+}
+
+MMLA_DEV void lds_order() { asm volatile("" ::: "memory"); }
+
+// In-place forward 512-point complex FFT of buf (one wave; LDS ops of a wave execute in order).
+// n = 64 n1 + 8 n2 + n3, k = k1 + 8 k2 + 64 k3; tw[m] = W512^m.
+MMLA_DEV void fft512(cd* buf, const cd* tw, int lane) {
+  cd v[8];
+  // pass 1: lane = 8 n2 + n3, DFT-8 over n1, x W512^(lane k1) -> buf[64 k1 + lane]
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = buf[64 * i + lane];
+  lds_order();
+  dft8(v);
+#pragma unroll
+  for (int k1 = 0; k1 < 8; ++k1) buf[64 * k1 + lane] = k1 ? cmul(v[k1], tw[(lane * k1) & 511]) : v[0];
+  lds_order();
+  // pass 2: lane = 8 k1 + n3, DFT-8 over n2 of buf[64 k1 + 8 n2 + n3], x W64^(n3 k2)
+  {
+    const int k1 = lane >> 3, n3 = lane & 7;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = buf[64 * k1 + 8 * i + n3];
+    lds_order();
+    dft8(v);
+#pragma unroll
+    for (int k2 = 0; k2 < 8; ++k2)
+      buf[64 * k1 + 8 * k2 + n3] = k2 ? cmul(v[k2], tw[(8 * n3 * k2) & 511]) : v[0];
+  }
+  lds_order();
+  // pass 3: lane = 8 k1 + k2, DFT-8 over n3 -> Z[k1 + 8 k2 + 64 k3]; written back in natural order
+  {
+    const int k1 = lane >> 3, k2 = lane & 7;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = buf[64 * k1 + 8 * k2 + i];
+    lds_order();
+    dft8(v);
+#pragma unroll
+    for (int k3 = 0; k3 < 8; ++k3) buf[k1 + 8 * k2 + 64 * k3] = v[k3];
+  }
+  lds_order();
+}
+
+MMLA_DEV double db_of_power(double p) { return 10.0 * log10(fmax(1e-40, p)); }
+
+// frame t of the item's buffer: 1024 centred samples, reflect at the buffer edges, zeros outside
+// the signal; returns whether any sample is nonzero (wave-uniform)
+MMLA_DEV bool load_frame(const NrArgs& a, const NrItem& it, int t, cd* buf, int lane) {
+  const float* y = a.y + it.sig_off;
+  const double* win = a.tables->win;
+  bool nz = false;
+#pragma unroll 4
+  for (int m = lane; m < NFFT / 2; m += NT) {
+    double v[2];
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      int64_t u = (int64_t)HOP * t - NFFT / 2 + 2 * m + e;     // buffer index before reflect
+      if (u < 0) u = -u;
+      if (u >= a.L) u = 2 * (a.L - 1) - u;
+      const int64_t i = it.i1 + u;                           // signal index
+      const double x = (i >= 0 && i < it.n) ? (double)y[i] : 0.0;
+      nz |= x != 0.0;
+      v[e] = x * win[2 * m + e];
+    }
+    buf[m] = cd{v[0], v[1]};
+  }
+  return __any(nz);
+}
+
+}  // namespace
+
+// ---- signal STFT: S, mask bits, frame max dB ------------------------------------------------------
+__global__ void __launch_bounds__(NT) nr_stft_kernel(NrArgs a) {
+  __shared__ cd buf[512];
+  const int lane = threadIdx.x;
+  const int64_t item = blockIdx.x / a.T;
+  const int t = (int)(blockIdx.x - item * a.T);
+  const NrItem it = a.items[item];
+  const NrTables& tb = *a.tables;
+  double2* S = a.S + (item * a.T + t) * NB;
+  uint8_t* bits = a.bits + (item * a.T + t) * NB;
+  double mx = -INFINITY;
+  if (!load_frame(a, it, t, buf, lane)) {
+    const double dz = db_of_power(0.0);
+    for (int k = lane; k < NB; k += NT) {
+      S[k] = double2{0.0, 0.0};
+      bits[k] = dz > (double)a.thresh[k];
+    }
+    mx = dz;
+  } else {
+    lds_order();
+    fft512(buf, tb.w512, lane);
+    // real split: X[k] = (Z[k] + conj Z[512-k]) / 2 - i W1024^k (Z[k] - conj Z[512-k]) / 2
+    for (int k = lane; k < NB; k += NT) {
+      const cd z = buf[k & 511], zr = buf[(512 - k) & 511];
+      const cd e = {0.5 * (z.x + zr.x), 0.5 * (z.y - zr.y)};
+      const cd o = {0.5 * (z.y + zr.y), -0.5 * (z.x - zr.x)};
+      const cd w = {tb.w1024[k][0], tb.w1024[k][1]};
+      const cd X = cadd(e, cmul(w, o));
+      S[k] = double2{X.x, X.y};
+      const double db = db_of_power(X.x * X.x + X.y * X.y);
+      bits[k] = db > (double)a.thresh[k];
+      mx = fmax(mx, db);
+    }
+  }
+  mx = wave_max(mx);
+  if (lane == 0) a.fmax[item * a.T + t] = mx;
+}
+
+// ---- smoothed mask x S -> inverse FFT -> windowed time-domain frame --------------------------------
+__global__ void __launch_bounds__(NT) nr_gate_kernel(NrArgs a) {
+  __shared__ cd buf[512];
+  __shared__ float mrow[NG_T][NB + NG_F];          // mask rows t-3..t+3, 16 zero bins each side
+  __shared__ double fsm[NG_T][NB];                  // frequency-smoothed rows
+  const int lane = threadIdx.x;
+  const int64_t item = blockIdx.x / a.T;
+  const int t = (int)(blockIdx.x - item * a.T);
+  // frames that reach the kept interior [keep0, keep0 + keep_len) of the buffer
+  const int64_t f_lo = (int64_t)HOP * t - NFFT / 2, f_hi = f_lo + NFFT;
+  if (f_hi <= a.keep0 || f_lo >= a.keep0 + a.keep_len) return;
+  const NrTables& tb = *a.tables;
+  constexpr int HF = NG_F / 2, HT = NG_T / 2;
+  // the item's max dB -> the top_db floor c; mask = dB > th  OR  c > th
+  double gm = -INFINITY;
+  for (int i = lane; i < a.T; i += NT) gm = fmax(gm, a.fmax[item * a.T + i]);
+  gm = wave_max(gm);
+  const double c = gm - 80.0;
+  const double p = a.prop_decrease;
+  for (int r = 0; r < NG_T; ++r) {
+    const int tr = t + r - HT;
+    const bool in = tr >= 0 && tr < a.T;
+    const uint8_t* br = a.bits + (item * a.T + (in ? tr : 0)) * NB;
+    for (int k = lane; k < NB + 2 * HF; k += NT) {
+      const int kb = k - HF;
+      float v = 0.0f;
+      if (in && kb >= 0 && kb < NB) {
+        const bool m = br[kb] || c > (double)a.thresh[kb];
+        v = (float)((m ? 1.0 : 0.0) * p + (1.0 - p));     // exact in float for p = 1 (0 / 1)
+      }
+      mrow[r][k] = v;
+    }
+  }
+  __syncthreads();
+  for (int r = 0; r < NG_T; ++r)
+    for (int k = lane; k < NB; k += NT) {
+      double s = 0.0;
+#pragma unroll
+      for (int j = 0; j < NG_F; ++j) s = fma(tb.gf[j], (double)mrow[r][k + j], s);
+      fsm[r][k] = s;
+    }
+  __syncthreads();
+  const double2* S = a.S + (item * a.T + t) * NB;
+  // gated spectrum -> Z[k] = E[k] + i O[k] of the inverse real FFT (k = 0..511)
+  for (int k = lane; k < 512; k += NT) {
+    double mk = 0.0, mr = 0.0;
+#pragma unroll
+    for (int j = 0; j < NG_T; ++j) {
+      mk = fma(tb.gt[j], fsm[j][k], mk);
+      mr = fma(tb.gt[j], fsm[j][512 - k], mr);
+    }
+    const double2 s0 = S[k], s1 = S[512 - k];
+    const cd X = {s0.x * mk, s0.y * mk}, Xr = {s1.x * mr, s1.y * mr};   // X[k], X[512 - k]
+    const cd e = {0.5 * (X.x + Xr.x), 0.5 * (X.y - Xr.y)};             // (X[k] + conj X[512-k]) / 2
+    const cd d = {0.5 * (X.x - Xr.x), 0.5 * (X.y + Xr.y)};             // (X[k] - conj X[512-k]) / 2
+    const cd wc = {tb.w1024[k][0], -tb.w1024[k][1]};                   // W1024^-k
+    const cd o = cmul(d, wc);                                          // O[k]
+    // conj(Z) for the forward FFT used as an inverse: Z = E + i O
+    const cd Z = {e.x - o.y, e.y + o.x};
+    buf[k] = cd{Z.x, -Z.y};
+  }
+  lds_order();
+  fft512(buf, tb.w512, lane);
+  // z[n] = conj(FFT(conj Z))[n] / 512 = x[2n] + i x[2n+1]; windowed frame to HBM
+  double* out = a.frames + (item * a.T + t) * NFFT;
+  for (int n = lane; n < 512; n += NT) {
+    const cd z = buf[n];
+    const double x0 = z.x * (1.0 / 512.0), x1 = -z.y * (1.0 / 512.0);
+    out[2 * n] = x0 * tb.win[2 * n];
+    out[2 * n + 1] = x1 * tb.win[2 * n + 1];
+  }
+}
+
+// ---- overlap-add, window-sum-square normalisation, float32 out -------------------------------------
+__global__ void nr_ola_kernel(NrArgs a) {
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t item = gid / a.keep_len;
+  if (item >= a.n_items) return;
+  const int64_t i = gid - item * a.keep_len;
+  const NrItem it = a.items[item];
+  if (i >= it.out_len) return;
+  const int64_t j = a.keep0 + i + NFFT / 2;            // index into the untrimmed istft signal
+  int64_t t0 = (j - (NFFT - 1) + HOP - 1) / HOP;
+  if (j - (NFFT - 1) < 0) t0 = 0;
+  int64_t t1 = j / HOP;
+  if (t1 > a.T - 1) t1 = a.T - 1;
+  double acc = 0.0, wss = 0.0;
+  for (int64_t t = t0; t <= t1; ++t) {
+    const int off = (int)(j - HOP * t);
+    acc += a.frames[(item * a.T + t) * NFFT + off];
+    const double w = a.tables->win[off];
+    wss += w * w;
+  }
+  if (wss > 2.2250738585072014e-308) acc /= wss;
+  a.out[it.out_off + i] = (float)acc;
+}
+
+// ---- noise profile ----------------------------------------------------------------------------
+// float32 like the reference: librosa.load gives float32, so stft -> complex64, |X| (hypotf),
+// square, 10 log10(max(1e-40, .)) in float32; the global max / top_db clamp and the per-bin
+// mean / std over frames follow in nr_noise_thresh_kernel.
+__global__ void __launch_bounds__(NT) nr_noise_db_kernel(const float* noise, int64_t m, int Tn,
+                                                         const NrTables* tables, float* db,
+                                                         float* fmaxv) {
+  __shared__ cd buf[512];
+  const int lane = threadIdx.x;
+  const int t = blockIdx.x;
+  const NrTables& tb = *tables;
+  for (int q = lane; q < 512; q += NT) {
+    double v[2];
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      int64_t u = (int64_t)HOP * t - NFFT / 2 + 2 * q + e;
+      if (u < 0) u = -u;
+      if (u >= m) u = 2 * (m - 1) - u;
+      v[e] = (double)noise[u] * tb.win[2 * q + e];
+    }
+    buf[q] = cd{v[0], v[1]};
+  }
+  lds_order();
+  fft512(buf, tb.w512, lane);
+  float mx = -INFINITY;
+  for (int k = lane; k < NB; k += NT) {
+    const cd z = buf[k & 511], zr = buf[(512 - k) & 511];
+    const cd e = {0.5 * (z.x + zr.x), 0.5 * (z.y - zr.y)};
+    const cd o = {0.5 * (z.y + zr.y), -0.5 * (z.x - zr.x)};
+    const cd w = {tb.w1024[k][0], tb.w1024[k][1]};
+    const cd X = cadd(e, cmul(w, o));
+    const float re = (float)X.x, im = (float)X.y;        // complex64 storage
+    const float mag = hypotf(re, im);
+    const float pw = mag * mag;
+    const float d = 10.0f * log10f(fmaxf(1e-40f, pw));
+    db[(int64_t)t * NB + k] = d;
+    mx = fmaxf(mx, d);
+  }
+  mx = wave_max(mx);
+  if (lane == 0) fmaxv[t] = mx;
+}
+
+__global__ void nr_noise_thresh_kernel(const float* db, const float* fmaxv, int Tn, float n_std,
+                                       float* thresh) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= NB) return;
+  float gm = -INFINITY;
+  for (int t = 0; t < Tn; ++t) gm = fmaxf(gm, fmaxv[t]);
+  const float c = gm - 80.0f;
+  double s = 0.0;
+  for (int t = 0; t < Tn; ++t) s += (double)fmaxf(db[(int64_t)t * NB + k], c);
+  const float mean = (float)(s / Tn);
+  double v = 0.0;
+  for (int t = 0; t < Tn; ++t) {
+    const float d = fmaxf(db[(int64_t)t * NB + k], c) - mean;
+    v += (double)d * (double)d;
+  }
+  const float sd = sqrtf((float)(v / Tn));
+  thresh[k] = mean + sd * n_std;
+}
+
+// ---- host --------------------------------------------------------------------------------------
+void nr_build_tables(NrTables* t, int sr) {
+  const double PI = 3.14159265358979323846;
+  for (int n = 0; n < NFFT; ++n) t->win[n] = 0.5 - 0.5 * cos(2.0 * PI * n / NFFT);
+  for (int m = 0; m < 512; ++m) {
+    t->w512[m].x = cos(2.0 * PI * m / 512.0);
+    t->w512[m].y = -sin(2.0 * PI * m / 512.0);
+  }
+  for (int k = 0; k < NB; ++k) {
+    t->w1024[k][0] = cos(2.0 * PI * k / 1024.0);
+    t->w1024[k][1] = -sin(2.0 * PI * k / 1024.0);
+  }
+  // noisereduce _smoothing_filter(n_grad_freq, n_grad_time) = outer(f, g) / sum: separable into
+  // f / sum(f) and g / sum(g) (SpectralGate._generate_mask_smoothing_filter: 500 Hz, 50 ms)
+  const int ngf = (int)(500.0 / (sr / (NFFT / 2.0))), ngt = (int)(50.0 / ((double)HOP / sr * 1000.0));
+  auto ramp = [](int ng, std::vector<double>& out) {
+    std::vector<double> v;
+    for (int i = 0; i < ng + 1; ++i) v.push_back((double)i / (ng + 1));         // linspace(0,1,ng+1,endpoint=False)
+    for (int i = 0; i < ng + 2; ++i) v.push_back(1.0 - (double)i / (ng + 1));   // linspace(1,0,ng+2)
+    out.assign(v.begin() + 1, v.end() - 1);
+  };
+  std::vector<double> f, g;
+  ramp(ngf, f);
+  ramp(ngt, g);
+  double sf = 0, sg = 0;
+  for (double v : f) sf += v;
+  for (double v : g) sg += v;
+  t->ngf = (int)f.size();
+  t->ngt = (int)g.size();
+  for (int j = 0; j < NG_F; ++j) t->gf[j] = j < (int)f.size() ? f[j] / sf : 0.0;
+  for (int j = 0; j < NG_T; ++j) t->gt[j] = j < (int)g.size() ? g[j] / sg : 0.0;
+}
+
+hipError_t nr_noise_launch(const float* noise, int64_t m, const NrTables* tables, float* db_scratch,
+                           float* fmax_scratch, float n_std, float* thresh, hipStream_t s) {
+  const int Tn = (int)(1 + m / HOP);
+  hipLaunchKernelGGL(nr_noise_db_kernel, dim3(Tn), dim3(NT), 0, s, noise, m, Tn, tables, db_scratch,
+                     fmax_scratch);
+  hipLaunchKernelGGL(nr_noise_thresh_kernel, dim3((NB + 63) / 64), dim3(64), 0, s, db_scratch,
+                     fmax_scratch, Tn, n_std, thresh);
+  return hipGetLastError();
+}
+
+hipError_t nr_gate_launch(const NrArgs& a, hipStream_t s) {
+  if (a.n_items <= 0) return hipSuccess;
+  const unsigned frames = (unsigned)(a.n_items * a.T);
+  hipLaunchKernelGGL(nr_stft_kernel, dim3(frames), dim3(NT), 0, s, a);
+  hipLaunchKernelGGL(nr_gate_kernel, dim3(frames), dim3(NT), 0, s, a);
+  const int64_t tot = a.n_items * a.keep_len;
+  hipLaunchKernelGGL(nr_ola_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
