@@ -53,7 +53,7 @@ def parse():
     ap.add_argument('--steps', type=int, default=3)
     ap.add_argument('--warmup', type=int, default=1)
     ap.add_argument('--workload', default='od_pipeline',
-                    choices=['od_pipeline', 'si_pipeline', 'od_features'])
+                    choices=['od_pipeline', 'si_pipeline', 'od_features', 'noise_gate'])
     ap.add_argument('--clips', type=int, default=None, help='clips per GPU')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-seconds', type=float, default=15.0)
@@ -114,6 +114,25 @@ def cpu_baseline_od(pcm_sample, gpu_norm, gpu_probs, W, budget_s):
         err_norm, err_prob
 
 
+def cpu_baseline_nr(y_sample, noise, gpu_out, budget_s):
+    """Oracle (numpy/scipy) noisereduce-2.0 stationary gate on a bounded sample of the clips."""
+    from oracle import noisereduce as onr
+    threads = int(os.environ.get('OMP_NUM_THREADS', os.cpu_count() or 1))
+    n_done, err = 0, 0.0
+    t0 = time.perf_counter()
+    for i in range(len(y_sample)):
+        w = onr.reduce_noise(y_sample[i], 16000, noise)
+        err = max(err, float(np.abs(gpu_out[i] - w).max()))
+        n_done += 1
+        if time.perf_counter() - t0 > budget_s:
+            break
+    dt = time.perf_counter() - t0
+    return {'value': n_done / dt, 'unit': 'clips/s', 'cores': threads, 'kind': 'port',
+            'sample': f'{n_done} x 2.5 s synthetic clips, one call each (record_on_pc.py shape): numpy '
+                      f'librosa-0.8 stft/istft + scipy fftconvolve restatement of noisereduce 2.0 '
+                      f'(BLAS threads={threads})'}, err
+
+
 def cpu_baseline_si(pcm_sample, gpu_feat, gpu_probs, W, budget_s):
     from oracle import nets, si_fe
     threads = int(os.environ.get('OMP_NUM_THREADS', os.cpu_count() or 1))
@@ -149,6 +168,9 @@ def main():
     if wl == 'od_features':
         clips = args.clips or 4096
         clip_len = 40000
+    elif wl == 'noise_gate':
+        clips = args.clips or 4096
+        clip_len = 40000
     elif wl == 'si_pipeline':
         clips = args.clips or 65536
         clip_len = 24000
@@ -164,6 +186,15 @@ def main():
         ctx.load_weights(weights.SI, weights.pack(weights.SI, W_si, 630), 630, _lib.HEAD_SOFTMAX)
 
     pcm = make_clips(clips, clip_len, start_index=rank * clips)
+    if wl == 'noise_gate':   # float32 audio as librosa.load gives it, and a 10 s ambient-noise clip
+        yf = (pcm.float() / 32768.0).contiguous()
+        del pcm
+        pcm = None
+        gen = torch.Generator(device='cuda')
+        gen.manual_seed(4242)
+        noise_clip = (0.01 * torch.randn(160000, generator=gen, device='cuda')).cpu().numpy()
+        ctx.nr_set_noise(noise_clip)
+        nr_out = torch.empty_like(yf)
     K = 2 if wl == 'od_pipeline' else 630
     probs = torch.empty((clips, K), dtype=torch.float32, device='cuda')
     argmax = torch.empty(clips, dtype=torch.int32, device='cuda')
@@ -178,10 +209,12 @@ def main():
         elif wl == 'si_pipeline':
             ctx.si_pipeline_dev(pcm.data_ptr(), clips, clip_len, clip_len, probs.data_ptr(),
                                 argmax.data_ptr())
+        elif wl == 'noise_gate':
+            ctx.nr_reduce_dev(yf.data_ptr(), clips, clip_len, clip_len, nr_out.data_ptr())
         else:
             ctx.od_features_dev(pcm.data_ptr(), clips, clip_len, clip_len, norm=norm.data_ptr(),
                                 zcr=zcr.data_ptr())
-        if world > 1 and wl != 'od_features':
+        if world > 1 and wl not in ('od_features', 'noise_gate'):
             import torch.distributed as dist
             dist.all_gather_into_tensor(gathered, probs)   # RCCL over xGMI: logits to every rank
 
@@ -206,7 +239,7 @@ def main():
     # dominant kernel and its roofline (algorithmic work / device time from HIP events)
     stage = max(prof, key=lambda s: prof[s][0])
     ms, launches, work = prof[stage]
-    if stage in ('od_fe', 'si_fe'):
+    if stage in ('od_fe', 'si_fe', 'nr'):
         achieved = work / (ms * 1e-3) / 1e9
         roof = {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                 'frac': achieved / HBM_PEAK_GBS, 'traffic': None}
@@ -220,8 +253,8 @@ def main():
                  'work_per_launch': work / max(launches, 1)})
     roof['traffic'], roof['traffic_source'] = pmc_traffic(wl, stage, clips)
     stages = {s: {'ms': round(v[0], 3), 'launches': v[1],
-                  ('GB/s' if s in ('od_fe', 'si_fe') else 'TFLOP/s'):
-                      round(v[2] / (v[0] * 1e-3) / (1e9 if s in ('od_fe', 'si_fe') else 1e12), 3)
+                  ('GB/s' if s in ('od_fe', 'si_fe', 'nr') else 'TFLOP/s'):
+                      round(v[2] / (v[0] * 1e-3) / (1e9 if s in ('od_fe', 'si_fe', 'nr') else 1e12), 3)
                       if v[0] > 0 else 0.0}
               for s, v in prof.items() if v[1]}
 
@@ -251,8 +284,12 @@ def main():
     parity = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         n_s = 64
-        sample = pcm[:n_s].cpu().numpy()
-        if wl == 'si_pipeline':
+        sample = pcm[:n_s].cpu().numpy() if pcm is not None else None
+        if wl == 'noise_gate':
+            cpu, e1 = cpu_baseline_nr(yf[:n_s].cpu().numpy(), noise_clip, nr_out[:n_s].cpu().numpy(),
+                                      args.cpu_seconds)
+            parity = {'nr_max_abs_err_vs_oracle': e1}
+        elif wl == 'si_pipeline':
             feat = torch.empty((n_s, 256, 39), dtype=torch.float32, device='cuda')
             ctx.si_features_dev(pcm.data_ptr(), n_s, clip_len, clip_len, feat.data_ptr())
             torch.cuda.synchronize()
@@ -276,6 +313,8 @@ def main():
             'si_pipeline': 'config 4: MFCC+d+dd (float64) -> SI-NET Conv1D ResNet+BiLSTM -> '
                            'Dense(630) softmax, per GPU',
             'od_features': 'config 2: OD front-end kernel only (log-mel norm + ZCR out)',
+            'noise_gate': 'SURVEY 8f row 3: nr.reduce_noise(stationary=True) gate on 2.5 s clips '
+                          '(noisereduce 2.0 defaults, float64 STFT), per GPU',
         }[wl]
         line = {
             'metric': METRIC, 'value': value, 'unit': 'clips/s', 'n_gpus': world,
@@ -283,10 +322,14 @@ def main():
             'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
             # convolutions: error-compensated 3xFP16 on f16 MFMA with f32 accumulation; front-ends
             # f32 (OD) / f64 (SI); LSTM, heads f32
-            'dtype': 'f16x3+f32' if wl == 'od_pipeline' else ('f64+f16x3' if wl == 'si_pipeline' else 'f32'),
-            'data': f'synthetic: {clips} x {clip_len / 16000:g} s 16 kHz int16 clips per GPU generated '
-                    f'in HBM (5 classes, SURVEY 8d); seeded synthetic weights in the reference '
-                    f'variables.index layout (trained blobs absent)',
+            'dtype': {'od_pipeline': 'f16x3+f32', 'si_pipeline': 'f64+f16x3',
+                      'noise_gate': 'f64'}.get(wl, 'f32'),
+            'data': (f'synthetic: {clips} x {clip_len / 16000:g} s 16 kHz clips per GPU generated in '
+                     f'HBM (5 classes, SURVEY 8d)' +
+                     (', as float32 audio, gated against a 10 s synthetic noise profile'
+                      if wl == 'noise_gate' else
+                      ' (int16); seeded synthetic weights in the reference variables.index layout '
+                      '(trained blobs absent)')),
             'config': {'workload': f'{wl} ({desc})', 'clips_per_gpu': clips,
                        'global_batch': world * clips, 'clip_samples': clip_len,
                        'parallelism': f'dp{world}' + ('+rccl_allgather_logits' if world > 1 else '')},

@@ -210,7 +210,7 @@ int ws_get(mmla_ctx* c, int slot, size_t bytes, void** out) {
 enum Slot {
   S_PCM = 0, S_LENS, S_IMG, S_X, S_T1, S_T2, S_T3, S_SEQ, S_HOUT, S_LOGIT, S_FEAT, S_SILENT,
   S_OUT0, S_OUT1, S_OUT2, S_OUT3, S_IN, S_FESCR,
-  S_NR_S, S_NR_BITS, S_NR_FMAX, S_NR_FRAMES, S_NR_ITEMS, S_NR_Y
+  S_NR_S, S_NR_BITS, S_NR_FMAX, S_NR_FRAMES, S_NR_ITEMS, S_NR_Y, S_NR_ROWS
 };
 
 // ---- weights -------------------------------------------------------------------------------------
@@ -828,7 +828,7 @@ int mmla_nr_reduce(mmla_ctx* c, const float* y, int64_t n_signals, int64_t strid
   const int64_t L = keep + 2 * kNrPadding;
   const int T = (int)(1 + L / NR_HOP);
   const int64_t bins = NR_NFFT / 2 + 1;
-  const int64_t cap = std::max<int64_t>(1, std::min<int64_t>(kNrItemsPerLaunch, (int64_t)(2e10 / ((double)T * (bins * 17 + NR_NFFT * 8 + 8)))));
+  const int64_t cap = std::max<int64_t>(1, std::min<int64_t>(kNrItemsPerLaunch, (int64_t)(2e10 / ((double)T * (bins * 25 + NR_NFFT * 8 + 8)))));
   std::vector<NrItem> items;
   items.reserve(n_signals * per);
   for (int64_t sgl = 0; sgl < n_signals; ++sgl)
@@ -852,12 +852,13 @@ int mmla_nr_reduce(mmla_ctx* c, const float* y, int64_t n_signals, int64_t strid
   }
   for (size_t i0 = 0; i0 < items.size(); i0 += cap) {
     const int64_t ni = std::min<int64_t>(cap, (int64_t)items.size() - (int64_t)i0);
-    void *pS, *pB, *pM, *pF, *pI;
+    void *pS, *pB, *pM, *pF, *pI, *pR;
     CHK(ws_get(c, S_NR_S, (size_t)ni * T * bins * sizeof(double2), &pS));
     CHK(ws_get(c, S_NR_BITS, (size_t)ni * T * bins, &pB));
     CHK(ws_get(c, S_NR_FMAX, (size_t)ni * T * sizeof(double), &pM));
     CHK(ws_get(c, S_NR_FRAMES, (size_t)ni * T * NR_NFFT * sizeof(double), &pF));
     CHK(ws_get(c, S_NR_ITEMS, (size_t)ni * sizeof(NrItem), &pI));
+    CHK(ws_get(c, S_NR_ROWS, (size_t)ni * T * bins * sizeof(double), &pR));
     HIPCHK(c, hipMemcpyAsync(pI, items.data() + i0, ni * sizeof(NrItem), hipMemcpyHostToDevice,
                              c->stream));
     NrArgs a{};
@@ -875,6 +876,7 @@ int mmla_nr_reduce(mmla_ctx* c, const float* y, int64_t n_signals, int64_t strid
     a.bits = static_cast<uint8_t*>(pB);
     a.fmax = static_cast<double*>(pM);
     a.frames = static_cast<double*>(pF);
+    a.rows = static_cast<double*>(pR);
     a.out = dout;
     double bytes = 0;
     for (int64_t i = 0; i < ni; ++i) bytes += 8.0 * items[i0 + i].out_len;   // f32 in + f32 out

@@ -13,11 +13,12 @@
 //                      of the even/odd-packed frame (radix 8 x 8 x 8 in LDS) + real split -> S[513]
 //                      (complex128 to HBM), mask bit dB > thresh per bin, the frame's max dB; frames
 //                      whose window only covers zeros skip the FFT (S = 0, dB = 10 log10(1e-40))
-//   nr_gate_kernel     one wave per (item, frame) touching the kept interior: the item's max dB,
-//                      mask rows t-3..t+3 OR'ed with (max - 80 > thresh) (top_db clamp), the
-//                      33 x 7 smoothing filter (separable: freq then time, zero outside the array
-//                      like fftconvolve 'same'), S * mask, inverse real FFT, x window -> the frame
-//                      in the time domain (HBM scratch)
+//   nr_rows_kernel     one wave per (item, frame) within 3 frames of the kept interior: the item's
+//                      max dB, the frame's mask row OR'ed with (max - 80 > thresh) (top_db clamp),
+//                      smoothed over frequency (33 taps; the filter is separable) -> HBM row
+//   nr_gate_kernel     one wave per (item, frame) touching the kept interior: the time smoothing
+//                      of rows t-3..t+3 (7 taps, zero outside the array like fftconvolve 'same'),
+//                      S * mask, inverse real FFT, x window -> the frame in the time domain
 //   nr_ola_kernel      overlap-add of the <= 4 frames covering each kept sample, / window
 //                      sum-square, float32 out
 // The noise profile (per-bin threshold) is computed once per noise clip by nr_noise_db_kernel +
@@ -145,11 +146,13 @@ __global__ void __launch_bounds__(NT) nr_stft_kernel(NrArgs a) {
   uint8_t* bits = a.bits + (item * a.T + t) * NB;
   double mx = -INFINITY;
   if (!load_frame(a, it, t, buf, lane)) {
+    // a window of zeros: S = 0 is never read (nr_gate_kernel only reads frames that reach the
+    // kept interior, which overlap the signal); its mask bits are read by the smoothing rows of
+    // frames within NG_T / 2 of those
     const double dz = db_of_power(0.0);
-    for (int k = lane; k < NB; k += NT) {
-      S[k] = double2{0.0, 0.0};
-      bits[k] = dz > (double)a.thresh[k];
-    }
+    const int64_t f_lo = (int64_t)HOP * (t - NG_T / 2) - NFFT / 2, f_hi = (int64_t)HOP * (t + NG_T / 2) + NFFT / 2;
+    if (f_lo < a.keep0 + a.keep_len && f_hi > a.keep0)
+      for (int k = lane; k < NB; k += NT) bits[k] = dz > (double)a.thresh[k];
     mx = dz;
   } else {
     lds_order();
@@ -171,57 +174,75 @@ __global__ void __launch_bounds__(NT) nr_stft_kernel(NrArgs a) {
   if (lane == 0) a.fmax[item * a.T + t] = mx;
 }
 
-// ---- smoothed mask x S -> inverse FFT -> windowed time-domain frame --------------------------------
-__global__ void __launch_bounds__(NT) nr_gate_kernel(NrArgs a) {
-  __shared__ cd buf[512];
-  __shared__ float mrow[NG_T][NB + NG_F];          // mask rows t-3..t+3, 16 zero bins each side
-  __shared__ double fsm[NG_T][NB];                  // frequency-smoothed rows
+// frames whose smoothed mask the gate needs: those within NG_T / 2 of a frame reaching the kept
+// interior [keep0, keep0 + keep_len) of the buffer
+MMLA_DEV bool reaches(const NrArgs& a, int64_t t, int halo) {
+  const int64_t f_lo = (int64_t)HOP * (t - halo) - NFFT / 2, f_hi = (int64_t)HOP * (t + halo) + NFFT / 2;
+  return f_lo < a.keep0 + a.keep_len && f_hi > a.keep0;
+}
+
+// ---- mask row (dB > th OR top_db floor > th), smoothed over frequency: once per frame ---------------
+__global__ void __launch_bounds__(NT) nr_rows_kernel(NrArgs a) {
+  __shared__ float mrow[NB + NG_F];                 // 16 zero bins each side
   const int lane = threadIdx.x;
   const int64_t item = blockIdx.x / a.T;
   const int t = (int)(blockIdx.x - item * a.T);
-  // frames that reach the kept interior [keep0, keep0 + keep_len) of the buffer
-  const int64_t f_lo = (int64_t)HOP * t - NFFT / 2, f_hi = f_lo + NFFT;
-  if (f_hi <= a.keep0 || f_lo >= a.keep0 + a.keep_len) return;
+  if (!reaches(a, t, NG_T / 2)) return;
   const NrTables& tb = *a.tables;
-  constexpr int HF = NG_F / 2, HT = NG_T / 2;
-  // the item's max dB -> the top_db floor c; mask = dB > th  OR  c > th
+  constexpr int HF = NG_F / 2;
+  // the item's max dB -> the top_db floor c; mask = max(dB, c) > th = (dB > th) | (c > th)
   double gm = -INFINITY;
   for (int i = lane; i < a.T; i += NT) gm = fmax(gm, a.fmax[item * a.T + i]);
   gm = wave_max(gm);
   const double c = gm - 80.0;
   const double p = a.prop_decrease;
-  for (int r = 0; r < NG_T; ++r) {
-    const int tr = t + r - HT;
-    const bool in = tr >= 0 && tr < a.T;
-    const uint8_t* br = a.bits + (item * a.T + (in ? tr : 0)) * NB;
-    for (int k = lane; k < NB + 2 * HF; k += NT) {
-      const int kb = k - HF;
-      float v = 0.0f;
-      if (in && kb >= 0 && kb < NB) {
-        const bool m = br[kb] || c > (double)a.thresh[kb];
-        v = (float)((m ? 1.0 : 0.0) * p + (1.0 - p));     // exact in float for p = 1 (0 / 1)
-      }
-      mrow[r][k] = v;
+  const uint8_t* br = a.bits + (item * a.T + t) * NB;
+  for (int k = lane; k < NB + 2 * HF; k += NT) {
+    const int kb = k - HF;
+    float v = 0.0f;
+    if (kb >= 0 && kb < NB) {
+      const bool m = br[kb] || c > (double)a.thresh[kb];
+      v = (float)((m ? 1.0 : 0.0) * p + (1.0 - p));     // exact in float for p = 1 (0 / 1)
     }
+    mrow[k] = v;
   }
-  __syncthreads();
-  for (int r = 0; r < NG_T; ++r)
-    for (int k = lane; k < NB; k += NT) {
-      double s = 0.0;
+  lds_order();
+  double* row = a.rows + (item * a.T + t) * NB;
+  for (int k = lane; k < NB; k += NT) {
+    double sacc = 0.0;
 #pragma unroll
-      for (int j = 0; j < NG_F; ++j) s = fma(tb.gf[j], (double)mrow[r][k + j], s);
-      fsm[r][k] = s;
-    }
-  __syncthreads();
+    for (int j = 0; j < NG_F; ++j) sacc = fma(tb.gf[j], (double)mrow[k + j], sacc);
+    row[k] = sacc;
+  }
+}
+
+// ---- time smoothing of the rows x S -> inverse FFT -> windowed time-domain frame ------------------
+__global__ void __launch_bounds__(NT) nr_gate_kernel(NrArgs a) {
+  __shared__ cd buf[512];
+  const int lane = threadIdx.x;
+  const int64_t item = blockIdx.x / a.T;
+  const int t = (int)(blockIdx.x - item * a.T);
+  if (!reaches(a, t, 0)) return;
+  const NrTables& tb = *a.tables;
+  constexpr int HT = NG_T / 2;
+  const double* rows[NG_T];                          // rows t-3..t+3 (zero outside [0, T))
+  bool rin[NG_T];
+#pragma unroll
+  for (int j = 0; j < NG_T; ++j) {
+    const int tr = t + j - HT;
+    rin[j] = tr >= 0 && tr < a.T;
+    rows[j] = a.rows + (item * a.T + (rin[j] ? tr : 0)) * NB;
+  }
   const double2* S = a.S + (item * a.T + t) * NB;
   // gated spectrum -> Z[k] = E[k] + i O[k] of the inverse real FFT (k = 0..511)
   for (int k = lane; k < 512; k += NT) {
     double mk = 0.0, mr = 0.0;
 #pragma unroll
-    for (int j = 0; j < NG_T; ++j) {
-      mk = fma(tb.gt[j], fsm[j][k], mk);
-      mr = fma(tb.gt[j], fsm[j][512 - k], mr);
-    }
+    for (int j = 0; j < NG_T; ++j)
+      if (rin[j]) {
+        mk = fma(tb.gt[j], rows[j][k], mk);
+        mr = fma(tb.gt[j], rows[j][512 - k], mr);
+      }
     const double2 s0 = S[k], s1 = S[512 - k];
     const cd X = {s0.x * mk, s0.y * mk}, Xr = {s1.x * mr, s1.y * mr};   // X[k], X[512 - k]
     const cd e = {0.5 * (X.x + Xr.x), 0.5 * (X.y - Xr.y)};             // (X[k] + conj X[512-k]) / 2
@@ -376,6 +397,7 @@ hipError_t nr_gate_launch(const NrArgs& a, hipStream_t s) {
   if (a.n_items <= 0) return hipSuccess;
   const unsigned frames = (unsigned)(a.n_items * a.T);
   hipLaunchKernelGGL(nr_stft_kernel, dim3(frames), dim3(NT), 0, s, a);
+  hipLaunchKernelGGL(nr_rows_kernel, dim3(frames), dim3(NT), 0, s, a);
   hipLaunchKernelGGL(nr_gate_kernel, dim3(frames), dim3(NT), 0, s, a);
   const int64_t tot = a.n_items * a.keep_len;
   hipLaunchKernelGGL(nr_ola_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, a);
