@@ -50,6 +50,20 @@ MMLA_DEV float pro_fn(float v, float sc, float sh) {
   }
 }
 
+// Pixels per tile.  BN 64 tiles of 256 pixels stage B once per 256 pixels and cut the halo share
+// (measured: <3,3,64,8> 1.88 -> 1.51 ms, <4,1,64,16,pool> 4.01 -> 3.62, <4,1,64,8,res> 1.27 -> 1.20)
+// at occupancy 2; the 3x3 TW 16 variant is slower with them (3.31 -> 3.54) and keeps 128.  BN 128
+// halved to 64 pixels (occupancy 4) was 25-33 % slower: per-tile costs dominate, not latency.
+template <int KH, int BN, int TW>
+constexpr int tile_px() { return BN == 64 && TW > 1 && !(KH == 3 && TW == 16) ? 256 : BM; }
+
+// TW == 0 (LIN): a tile is 128 consecutive pixels of the whole batch in NHWC order (rows of all
+// clips back to back), so the 19-wide images do not pad 19 -> 24 columns.  The rows the tile touches
+// plus the halo rows are staged with a padded pitch of w + kw - 1 pixels (<= LIN_WP) into at most
+// LIN_SLOTS row slots; a tap whose source row lies outside the output pixel's clip reads row slot
+// LIN_SLOTS, which stays zero.
+constexpr int LIN_SLOTS = 11, LIN_WP = 21;
+
 // V4: channels loaded as float4 (cin % 4 == 0); else per element (the SI stem, cin = 39).
 // PIN (Conv1D): the input rows are MaxPool1D(2, 'same') of x, taken while staging (SI pool units)
 template <int KH, int KW, int CK, int BN, int TW, int PRO, int EPI, bool POOL, bool V4 = true,
@@ -59,15 +73,18 @@ __global__ void __launch_bounds__(NT, 2) conv_h3_kernel(ConvH3Args a) {
   // 128 / WM rows: BN 32 -> 4 x 1, BN 64 -> 2 x 2, BN 128 -> 1 x 4 (waves along N)
   constexpr int WN = BN / 32;
   constexpr int WM = 4 / WN;
-  constexpr int MT = BM / (WM * 32);      // 32-row tiles per wave
+  constexpr int BMK = tile_px<KH, BN, TW>();
+  constexpr int MT = BMK / (WM * 32);     // 32-row tiles per wave
   constexpr int NTL = BN / (WN * 32);     // 32-col tiles per wave
   constexpr int LDP = CK + 8;             // fp16 per staged pixel (16-B pad)
   constexpr int KS = CK / 16;             // MFMA k-steps per chunk
   constexpr int TAPS = KH * KW;
-  constexpr int TH = BM / TW;
-  constexpr int WP = TW + KW - 1;
-  constexpr int HP = TH + KH - 1;
+  constexpr bool LIN = TW == 0;
+  constexpr int TH = LIN ? 0 : BMK / (LIN ? 1 : TW);
+  constexpr int WP = LIN ? LIN_WP : TW + KW - 1;
+  constexpr int HP = LIN ? LIN_SLOTS + 1 : TH + KH - 1;   // LIN: + the zero row
   constexpr int NPIX = HP * WP;
+  constexpr int NSTG = LIN ? LIN_SLOTS * LIN_WP : NPIX;   // staged pixels (upper bound)
   constexpr int QPP = CK / 4;             // float4 per staged pixel
   __shared__ __attribute__((aligned(16))) _Float16 lds_hi[NPIX * LDP];
   __shared__ __attribute__((aligned(16))) _Float16 lds_lo[NPIX * LDP];
@@ -76,9 +93,9 @@ __global__ void __launch_bounds__(NT, 2) conv_h3_kernel(ConvH3Args a) {
   const int wm = wave / WN, wn = wave - (wave / WN) * WN;
   // TW == 1 (Conv1D): the clips' rows form ONE sequence of n * h rows tiled 128 at a time, so a
   // short sequence (t = 64, 32) does not pad a tile; taps that cross a clip boundary read zeros
-  const int HH = TW == 1 ? a.n * a.h : a.h;
+  const int HH = TW <= 1 ? a.n * a.h : a.h;
   const int tiles = a.tiles_h * a.tiles_w;
-  const int64_t clip = TW == 1 ? 0 : blockIdx.x / tiles;
+  const int64_t clip = TW <= 1 ? 0 : blockIdx.x / tiles;
   const int tile = blockIdx.x - (int)(clip * tiles);
   const int th_i = tile / a.tiles_w;
   const int h0 = th_i * TH;
@@ -89,11 +106,35 @@ __global__ void __launch_bounds__(NT, 2) conv_h3_kernel(ConvH3Args a) {
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
     const int m = (wm * MT + mt) * 32 + (lane & 31);
-    apix[mt] = ((m / TW) * WP + (m % TW)) * LDP;
+    apix[mt] = LIN ? 0 : ((m / (LIN ? 1 : TW)) * WP + (m % (LIN ? 1 : TW))) * LDP;
   }
   int trow[MT];   // TW == 1: the A row's position inside its clip
 #pragma unroll
-  for (int mt = 0; mt < MT; ++mt) trow[mt] = (h0 + (wm * MT + mt) * 32 + (lane & 31)) % a.h;
+  for (int mt = 0; mt < MT; ++mt) trow[mt] = TW == 1 ? (h0 + (wm * MT + mt) * 32 + (lane & 31)) % a.h : 0;
+  // LIN: p0 = first pixel of the tile (flattened over n * h * w), r0 = its row; per A row and
+  // kernel row dy the LDS pixel of tap (dy, 0), or the zero row when the source row leaves the clip
+  const int wpad = a.w + KW - 1;
+  const int64_t npx = (int64_t)a.n * a.h * a.w;
+  const int64_t p0 = LIN ? (int64_t)tile * BMK : 0;
+  const int r0 = LIN ? (int)(p0 / a.w) : 0;
+  int abase[MT][LIN ? KH : 1];
+  if constexpr (LIN) {
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const int64_t P = p0 + (wm * MT + mt) * 32 + (lane & 31);
+      const int r = (int)(P / a.w), c = (int)(P - (int64_t)r * a.w), cr = r % a.h;
+#pragma unroll
+      for (int dy = 0; dy < KH; ++dy) {
+        const int sr = cr + dy - a.pad_h;
+        abase[mt][dy] = ((sr >= 0 && sr < a.h ? (r - r0 + dy) * wpad : LIN_SLOTS * wpad) + c) * LDP;
+      }
+    }
+    // the zero row (never staged)
+    for (int i = tid; i < LIN_WP * QPP; i += NT) {
+      *reinterpret_cast<f16x4*>(lds_hi + (LIN_SLOTS * wpad + i / QPP) * LDP + (i % QPP) * 4) = f16x4{};
+      *reinterpret_cast<f16x4*>(lds_lo + (LIN_SLOTS * wpad + i / QPP) * LDP + (i % QPP) * 4) = f16x4{};
+    }
+  }
   const int koff = (lane >> 5) * 8;
 
   f32x16 acc1[MT][NTL], acc2[MT][NTL];
@@ -125,17 +166,18 @@ __global__ void __launch_bounds__(NT, 2) conv_h3_kernel(ConvH3Args a) {
     // ---- stage the input halo of this channel chunk: prologue once per element, split hi/lo ----
     // all of this thread's halo loads are issued before the first is consumed (one HBM latency
     // per chunk, not one per element group)
-    constexpr int MAXT = (NPIX * QPP + NT - 1) / NT;
+    constexpr int MAXT = (NSTG * QPP + NT - 1) / NT;
+    const int nstg = LIN ? LIN_SLOTS * wpad : NPIX;
     float4 pre[MAXT];
     uint32_t valid = 0;
 #pragma unroll
     for (int j = 0; j < MAXT; ++j) {
       const int task = tid + j * NT;
       pre[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (task < NPIX * QPP) {
+      if (task < nstg * QPP) {
         const int px = task / QPP, q = task % QPP;
-        const int py = px / WP, pxx = px % WP;
-        const int ih = h0 - a.pad_h + py, iw = w0 - a.pad_w + pxx;
+        const int py = LIN ? px / wpad : px / WP, pxx = LIN ? px - py * wpad : px % WP;
+        const int ih = (LIN ? r0 : h0) - a.pad_h + py, iw = w0 - a.pad_w + pxx;
         const int ci = ci0 + q * 4;
         if (ih >= 0 && ih < HH && iw >= 0 && iw < a.w && ci < a.cin) {
           const float* src = xclip + (ih * a.w + iw) * a.cin + ci;
@@ -164,7 +206,7 @@ __global__ void __launch_bounds__(NT, 2) conv_h3_kernel(ConvH3Args a) {
 #pragma unroll
     for (int j = 0; j < MAXT; ++j) {
       const int task = tid + j * NT;
-      if (task >= NPIX * QPP) continue;
+      if (task >= nstg * QPP) continue;
       const int px = task / QPP, q = task % QPP;
       const int ci = ci0 + q * 4;
       float4 v = pre[j];
@@ -221,7 +263,7 @@ __global__ void __launch_bounds__(NT, 2) conv_h3_kernel(ConvH3Args a) {
       for (int s = 0; s < KS; ++s) {
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
-          const int off = apix[mt] + toff + 16 * s + koff;
+          const int off = (LIN ? abase[mt][LIN ? dy : 0] + dx * LDP : apix[mt] + toff) + 16 * s + koff;
           f16x8 ah = *reinterpret_cast<const f16x8*>(lds_hi + off);
           f16x8 al = *reinterpret_cast<const f16x8*>(lds_lo + off);
           if constexpr (TW == 1 && KH > 1) {
@@ -267,7 +309,14 @@ __global__ void __launch_bounds__(NT, 2) conv_h3_kernel(ConvH3Args a) {
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const int m0 = mbase + 8 * g + hsel;
-          const int oh = h0 + m0 / TW, ow0 = w0 + m0 % TW;
+          if constexpr (LIN) {
+            const float* rp = a.res + (p0 + m0) * a.cout + co;
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              rsd[nt][mt][4 * g + j] = co < a.cout && p0 + m0 + j < npx ? rp[j * a.cout] : 0.0f;
+            continue;
+          }
+          const int oh = h0 + m0 / (LIN ? 1 : TW), ow0 = w0 + m0 % (LIN ? 1 : TW);
           const float* rp = a.res + ((clip * HH + oh) * a.w + ow0) * a.cout + co;
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
@@ -294,6 +343,7 @@ __global__ void __launch_bounds__(NT, 2) conv_h3_kernel(ConvH3Args a) {
         // windows: top-left rows i = 8q + hsel + e (i % TW even, (i / TW) even) -> registers
         // {4q+e, 4q+e+1, 4q+e+TW/2, 4q+e+TW/2+1}  (row + TW = register + TW/2)
         static_assert(TW == 16 || TW == 8, "pooled epilogue needs TW 8 or 16");
+        constexpr int TWP = TW == 16 ? 16 : 8;
         const int hp = (a.h + 1) >> 1, wp = (a.w + 1) >> 1;
 #pragma unroll
         for (int q = 0; q < 4; ++q)
@@ -301,10 +351,10 @@ __global__ void __launch_bounds__(NT, 2) conv_h3_kernel(ConvH3Args a) {
           for (int e = 0; e < 4; e += 2) {
             constexpr int R = TW / 2;
             const int i = 8 * q + hsel + e;
-            if ((i / TW) & 1) continue;                    // only top rows of window pairs
+            if ((i / TWP) & 1) continue;                   // only top rows of window pairs
             if (4 * q + e + R + 1 > 15) continue;
             const int m = mbase + i;
-            const int oh = h0 + m / TW, ow = w0 + m % TW;
+            const int oh = h0 + m / TWP, ow = w0 + m % TWP;
             if (oh >= a.h || ow >= a.w) continue;
             float mx = v[4 * q + e];
             if (ow + 1 < a.w) mx = fmaxf(mx, v[4 * q + e + 1]);
@@ -318,9 +368,20 @@ __global__ void __launch_bounds__(NT, 2) conv_h3_kernel(ConvH3Args a) {
 #pragma unroll
         for (int g = 0; g < 4; ++g) {        // 4 groups of 4 consecutive tile rows
           const int m0 = mbase + 8 * g + hsel;
-          const int oh = h0 + m0 / TW;
+          if constexpr (LIN) {               // 4 consecutive pixels of the flattened batch
+            float* yp = a.y + (p0 + m0) * a.cout + co;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              if (p0 + m0 + j >= npx) continue;
+              float val = v[4 * g + j];
+              if constexpr (EPI == EPI_ADD) val += rsd[nt][mt][4 * g + j];
+              yp[j * a.cout] = val;
+            }
+            continue;
+          }
+          const int oh = h0 + m0 / (LIN ? 1 : TW);
           if (oh >= HH) continue;
-          const int ow0 = w0 + m0 % TW;
+          const int ow0 = w0 + m0 % (LIN ? 1 : TW);
           float* yp = a.y + ((clip * HH + oh) * a.w + ow0) * a.cout + co;
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
@@ -340,8 +401,17 @@ __global__ void __launch_bounds__(NT, 2) conv_h3_kernel(ConvH3Args a) {
 
 template <int KH, int KW, int CK, int BN, int TW, int PRO, int EPI, bool POOL, bool V4 = true,
           bool PIN = false>
-hipError_t launch(const ConvH3Args& a, hipStream_t s) {
-  const int64_t tiles = (int64_t)a.tiles_h * a.tiles_w * (TW == 1 ? 1 : a.n);
+hipError_t launch(ConvH3Args a, hipStream_t s) {
+  constexpr int BMK = tile_px<KH, BN, TW>();
+  if constexpr (TW == 0) {
+    a.th = 0;
+    a.tiles_w = 1;
+    a.tiles_h = (int)(((int64_t)a.n * a.h * a.w + BMK - 1) / BMK);
+  } else {
+    a.th = BMK / TW;
+    a.tiles_h = TW == 1 ? (int)(((int64_t)a.n * a.h + a.th - 1) / a.th) : (a.h + a.th - 1) / a.th;
+  }
+  const int64_t tiles = (int64_t)a.tiles_h * a.tiles_w * (TW <= 1 ? 1 : a.n);
   dim3 grid((unsigned)tiles, (unsigned)(a.cout_pad / BN));
   hipLaunchKernelGGL((conv_h3_kernel<KH, KW, CK, BN, TW, PRO, EPI, POOL, V4, PIN>), grid, dim3(NT), 0,
                      s, a);
@@ -365,19 +435,21 @@ hipError_t conv_h3_launch(ConvH3Args a, hipStream_t s) {
     if (a.kh == 4 && a.kw == 1 && a.w == 1 && a.cin_pad % 16 == 0 && a.cout_pad == 32 &&
         a.pro == PRO_NONE && a.epi == EPI_BIAS && !a.pool_out) {
       a.tw = 1;
-      a.th = BM;
-      a.tiles_h = (int)(((int64_t)a.n * a.h + a.th - 1) / a.th);
       a.tiles_w = 1;
       return launch<4, 1, 16, 32, 1, PRO_NONE, EPI_BIAS, false, false>(a, s);
     }
     return hipErrorInvalidValue;
   }
   // tile: 16 wide for wide images, 8 for narrow ones (W = 38, 19), 1 for Conv1D
+  // (th, tiles_h follow from the variant's tile size in launch<>; Conv1D is one row sequence
+  // over all clips, conv_h3_kernel TW == 1)
   a.tw = a.w == 1 ? 1 : (a.w >= 48 ? 16 : 8);
-  a.th = BM / a.tw;
-  // Conv1D: one row sequence over all clips (conv_h3_kernel TW == 1)
-  a.tiles_h = a.tw == 1 ? (int)(((int64_t)a.n * a.h + a.th - 1) / a.th) : (a.h + a.th - 1) / a.th;
-  a.tiles_w = (a.w + a.tw - 1) / a.tw;
+  // narrow images whose 128-pixel tiles span few rows: linear-pixel tiles (TW = 0), no padding
+  // columns (W = 19: 8-wide tiles compute 24 columns for 19)
+  if (a.w > 1 && a.w < 24 && !a.pool_out && a.w + a.kw - 1 <= LIN_WP &&
+      (a.w - 1 + BM - 1) / a.w + a.kh <= LIN_SLOTS)
+    a.tw = 0;
+  a.tiles_w = a.tw == 0 ? 1 : (a.w + a.tw - 1) / a.tw;
   const int ck = a.cin_pad % 32 == 0 ? 32 : 16;
   if (a.cin_pad % ck != 0) return hipErrorInvalidValue;
   if (a.pool_in) {   // SI pool unit: MaxPool1D(2) -> BN -> ReLU -> Conv1D(3)
@@ -394,10 +466,12 @@ hipError_t conv_h3_launch(ConvH3Args a, hipStream_t s) {
   H3(3, 3, 16, 16, PRO_BN_ELU, EPI_BIAS, false)
   H3(3, 3, 32, 16, PRO_BN_ELU, EPI_BIAS, false)
   H3(3, 3, 32, 8, PRO_BN_ELU, EPI_BIAS, false)
+  H3(3, 3, 32, 0, PRO_BN_ELU, EPI_BIAS, false)
   H3(4, 1, 32, 16, PRO_BN_ELU, EPI_BIAS, true)
   H3(4, 1, 32, 8, PRO_BN_ELU, EPI_BIAS, true)
   H3(4, 1, 32, 16, PRO_BN_ELU, EPI_ADD, false)
   H3(4, 1, 32, 8, PRO_BN_ELU, EPI_ADD, false)
+  H3(4, 1, 32, 0, PRO_BN_ELU, EPI_ADD, false)
   // SI-NET res_unit convs (speaker_identification.py:173-188)
   H3(3, 1, 32, 1, PRO_BN_RELU, EPI_BIAS, false)
   H3(3, 1, 32, 1, PRO_BN_RELU, EPI_ADD, false)

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round measurement: the three bench workloads (default = the headline OD pipeline) + rocprof kernel
+# Round measurement: the four bench workloads (default = the headline OD pipeline) + rocprof kernel
 # stats of the OD pipeline.  Outputs under gpurun_out/ (copied into profiles/ by hand).
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
@@ -10,11 +10,13 @@ timeout -k 10 600 python3 bench.py --workload si_pipeline > gpurun_out/bench_si.
 grep '^{' gpurun_out/bench_si.json.log > gpurun_out/bench_si.json
 timeout -k 10 600 python3 bench.py --workload od_features > gpurun_out/bench_fe.json.log 2>&1 || exit $?
 grep '^{' gpurun_out/bench_fe.json.log > gpurun_out/bench_fe.json
+timeout -k 10 600 python3 bench.py --workload noise_gate > gpurun_out/bench_nr.json.log 2>&1 || exit $?
+grep '^{' gpurun_out/bench_nr.json.log > gpurun_out/bench_nr.json
 rm -rf gpurun_out/prof_bench
 timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_bench -o od -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/prof_bench.log 2>&1 || exit $?
 python3 - <<'PY'
 import json
-for f in ('od', 'si', 'fe'):
+for f in ('od', 'si', 'fe', 'nr'):
     d = json.load(open(f'gpurun_out/bench_{f}.json'))
     print(f, d['value'], d['unit'], 'ms/step', round(d['ms_per_step'], 2), 'roof', {k: d['roofline'][k] for k in ('kernel', 'achieved', 'peak', 'frac') if k in d['roofline']}, 'cpu', (d.get('cpu_baseline') or {}).get('value'))
 PY

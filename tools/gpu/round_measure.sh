@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round measurement: bench suite (3 workloads) + rocprof kernel stats (OD, SI) + PMC traffic
+# Round measurement: bench suite (4 workloads) + rocprof kernel stats (OD, SI) + PMC traffic
 cd $GRAFT_REPO_ROOT
 bash tools/gpu/bench_all.sh || exit $?
 bash tools/gpu/prof_si.sh || exit $?
