@@ -855,7 +855,7 @@ int mmla_nr_reduce(mmla_ctx* c, const float* y, int64_t n_signals, int64_t strid
     void *pS, *pB, *pM, *pF, *pI, *pR;
     CHK(ws_get(c, S_NR_S, (size_t)ni * T * bins * sizeof(double2), &pS));
     CHK(ws_get(c, S_NR_BITS, (size_t)ni * T * bins, &pB));
-    CHK(ws_get(c, S_NR_FMAX, (size_t)ni * T * sizeof(double), &pM));
+    CHK(ws_get(c, S_NR_FMAX, (size_t)ni * (T + 1) * sizeof(double), &pM));
     CHK(ws_get(c, S_NR_FRAMES, (size_t)ni * T * NR_NFFT * sizeof(double), &pF));
     CHK(ws_get(c, S_NR_ITEMS, (size_t)ni * sizeof(NrItem), &pI));
     CHK(ws_get(c, S_NR_ROWS, (size_t)ni * T * bins * sizeof(double), &pR));
@@ -875,6 +875,7 @@ int mmla_nr_reduce(mmla_ctx* c, const float* y, int64_t n_signals, int64_t strid
     a.S = static_cast<double2*>(pS);
     a.bits = static_cast<uint8_t*>(pB);
     a.fmax = static_cast<double*>(pM);
+    a.gmax = static_cast<double*>(pM) + ni * T;
     a.frames = static_cast<double*>(pF);
     a.rows = static_cast<double*>(pR);
     a.out = dout;

@@ -38,6 +38,7 @@ struct NrArgs {
   double2* S;                   // scratch [n_items][T][513] complex128
   uint8_t* bits;                // scratch [n_items][T][513] dB > thresh
   double* fmax;                 // scratch [n_items][T] frame max dB
+  double* gmax;                 // scratch [n_items] max over the item's frames
   double* rows;                 // scratch [n_items][T][513] frequency-smoothed mask rows
   double* frames;               // scratch [n_items][T][1024] gated windowed frames
   float* out;

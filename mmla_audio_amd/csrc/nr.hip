@@ -37,6 +37,7 @@ constexpr int HOP = NR_HOP;         // 256
 constexpr int NB = NFFT / 2 + 1;    // 513 bins
 constexpr int NG_F = NR_NGF;        // 33 frequency taps
 constexpr int NG_T = NR_NGT;        // 7 time taps
+constexpr int KPL = (NB + 63) / 64;  // bins per lane (k = lane + 64 i)
 
 // complex 8-point DFT in registers (W8^(nk)), in/out natural order
 MMLA_DEV void dft8(cd v[8]) {
@@ -73,13 +74,20 @@ MMLA_DEV void lds_order() { asm volatile("" ::: "memory"); }
 // n = 64 n1 + 8 n2 + n3, k = k1 + 8 k2 + 64 k3; tw[m] = W512^m.
 MMLA_DEV void fft512(cd* buf, const cd* tw, int lane) {
   cd v[8];
+  // this lane's 14 twiddles, all loads issued before the first pass
+  cd t1[8], t2[8];
+#pragma unroll
+  for (int k = 1; k < 8; ++k) {
+    t1[k] = tw[(lane * k) & 511];
+    t2[k] = tw[(8 * (lane & 7) * k) & 511];
+  }
   // pass 1: lane = 8 n2 + n3, DFT-8 over n1, x W512^(lane k1) -> buf[64 k1 + lane]
 #pragma unroll
   for (int i = 0; i < 8; ++i) v[i] = buf[64 * i + lane];
   lds_order();
   dft8(v);
 #pragma unroll
-  for (int k1 = 0; k1 < 8; ++k1) buf[64 * k1 + lane] = k1 ? cmul(v[k1], tw[(lane * k1) & 511]) : v[0];
+  for (int k1 = 0; k1 < 8; ++k1) buf[64 * k1 + lane] = k1 ? cmul(v[k1], t1[k1]) : v[0];
   lds_order();
   // pass 2: lane = 8 k1 + n3, DFT-8 over n2 of buf[64 k1 + 8 n2 + n3], x W64^(n3 k2)
   {
@@ -90,7 +98,7 @@ MMLA_DEV void fft512(cd* buf, const cd* tw, int lane) {
     dft8(v);
 #pragma unroll
     for (int k2 = 0; k2 < 8; ++k2)
-      buf[64 * k1 + 8 * k2 + n3] = k2 ? cmul(v[k2], tw[(8 * n3 * k2) & 511]) : v[0];
+      buf[64 * k1 + 8 * k2 + n3] = k2 ? cmul(v[k2], t2[k2]) : v[0];
   }
   lds_order();
   // pass 3: lane = 8 k1 + k2, DFT-8 over n3 -> Z[k1 + 8 k2 + 64 k3]; written back in natural order
@@ -106,6 +114,16 @@ MMLA_DEV void fft512(cd* buf, const cd* tw, int lane) {
   lds_order();
 }
 
+// Workgroups are dealt to the 8 XCDs round-robin (block b -> XCD b % 8): give each XCD one
+// contiguous range of the launch's frames, so neighbouring frames -- which share the overlapping
+// signal samples and the 7 smoothing rows -- meet in the same L2.  -1: past the last frame.
+constexpr int NXCD = 8;
+MMLA_DEV int64_t frame_of_block(const NrArgs& a) {
+  const int64_t total = a.n_items * a.T, per = (total + NXCD - 1) / NXCD;
+  const int64_t f = (int64_t)(blockIdx.x % NXCD) * per + blockIdx.x / NXCD;
+  return f < total ? f : -1;
+}
+
 MMLA_DEV double db_of_power(double p) { return 10.0 * log10(fmax(1e-40, p)); }
 
 // frame t of the item's buffer: 1024 centred samples, reflect at the buffer edges, zeros outside
@@ -114,7 +132,7 @@ MMLA_DEV bool load_frame(const NrArgs& a, const NrItem& it, int t, cd* buf, int 
   const float* y = a.y + it.sig_off;
   const double* win = a.tables->win;
   bool nz = false;
-#pragma unroll 4
+#pragma unroll
   for (int m = lane; m < NFFT / 2; m += NT) {
     double v[2];
 #pragma unroll
@@ -138,8 +156,10 @@ MMLA_DEV bool load_frame(const NrArgs& a, const NrItem& it, int t, cd* buf, int 
 __global__ void __launch_bounds__(NT) nr_stft_kernel(NrArgs a) {
   __shared__ cd buf[512];
   const int lane = threadIdx.x;
-  const int64_t item = blockIdx.x / a.T;
-  const int t = (int)(blockIdx.x - item * a.T);
+  const int64_t fr = frame_of_block(a);
+  if (fr < 0) return;
+  const int64_t item = fr / a.T;
+  const int t = (int)(fr - item * a.T);
   const NrItem it = a.items[item];
   const NrTables& tb = *a.tables;
   double2* S = a.S + (item * a.T + t) * NB;
@@ -155,18 +175,29 @@ __global__ void __launch_bounds__(NT) nr_stft_kernel(NrArgs a) {
       for (int k = lane; k < NB; k += NT) bits[k] = dz > (double)a.thresh[k];
     mx = dz;
   } else {
+    // the split's per-bin tables (bins k = lane + 64 i), loaded under the FFT
+    cd wk[KPL];
+    float th[KPL];
+#pragma unroll
+    for (int i = 0; i < KPL; ++i) {
+      const int k = min(lane + NT * i, NB - 1);
+      wk[i] = cd{tb.w1024[k][0], tb.w1024[k][1]};
+      th[i] = a.thresh[k];
+    }
     lds_order();
     fft512(buf, tb.w512, lane);
     // real split: X[k] = (Z[k] + conj Z[512-k]) / 2 - i W1024^k (Z[k] - conj Z[512-k]) / 2
-    for (int k = lane; k < NB; k += NT) {
+#pragma unroll
+    for (int i = 0; i < KPL; ++i) {
+      const int k = lane + NT * i;
+      if (k >= NB) continue;
       const cd z = buf[k & 511], zr = buf[(512 - k) & 511];
       const cd e = {0.5 * (z.x + zr.x), 0.5 * (z.y - zr.y)};
       const cd o = {0.5 * (z.y + zr.y), -0.5 * (z.x - zr.x)};
-      const cd w = {tb.w1024[k][0], tb.w1024[k][1]};
-      const cd X = cadd(e, cmul(w, o));
+      const cd X = cadd(e, cmul(wk[i], o));
       S[k] = double2{X.x, X.y};
       const double db = db_of_power(X.x * X.x + X.y * X.y);
-      bits[k] = db > (double)a.thresh[k];
+      bits[k] = db > (double)th[i];
       mx = fmax(mx, db);
     }
   }
@@ -181,47 +212,97 @@ MMLA_DEV bool reaches(const NrArgs& a, int64_t t, int halo) {
   return f_lo < a.keep0 + a.keep_len && f_hi > a.keep0;
 }
 
+// ---- the item's max dB over all frames (amplitude_to_db's top_db reference) -------------------------
+__global__ void __launch_bounds__(NT) nr_gmax_kernel(NrArgs a) {
+  const int64_t item = blockIdx.x;
+  double gm = -INFINITY;
+  for (int i = threadIdx.x; i < a.T; i += NT) gm = fmax(gm, a.fmax[item * a.T + i]);
+  gm = wave_max(gm);
+  if (threadIdx.x == 0) a.gmax[item] = gm;
+}
+
 // ---- mask row (dB > th OR top_db floor > th), smoothed over frequency: once per frame ---------------
 __global__ void __launch_bounds__(NT) nr_rows_kernel(NrArgs a) {
-  __shared__ float mrow[NB + NG_F];                 // 16 zero bins each side
+  __shared__ __attribute__((aligned(16))) float mrow[NB + NG_F];   // 16 zero bins each side
   const int lane = threadIdx.x;
-  const int64_t item = blockIdx.x / a.T;
-  const int t = (int)(blockIdx.x - item * a.T);
+  const int64_t fr = frame_of_block(a);
+  if (fr < 0) return;
+  const int64_t item = fr / a.T;
+  const int t = (int)(fr - item * a.T);
   if (!reaches(a, t, NG_T / 2)) return;
   const NrTables& tb = *a.tables;
   constexpr int HF = NG_F / 2;
-  // the item's max dB -> the top_db floor c; mask = max(dB, c) > th = (dB > th) | (c > th)
-  double gm = -INFINITY;
-  for (int i = lane; i < a.T; i += NT) gm = fmax(gm, a.fmax[item * a.T + i]);
-  gm = wave_max(gm);
-  const double c = gm - 80.0;
+  // the item's max dB (nr_gmax_kernel) -> the top_db floor c; mask = max(dB, c) > th
+  // = (dB > th) | (c > th)
+  const double c = a.gmax[item] - 80.0;
   const double p = a.prop_decrease;
   const uint8_t* br = a.bits + (item * a.T + t) * NB;
-  for (int k = lane; k < NB + 2 * HF; k += NT) {
-    const int kb = k - HF;
+  constexpr int MPL = (NB + 2 * HF + NT - 1) / NT;   // 9
+  uint8_t bv[MPL];
+  float thv[MPL];
+#pragma unroll
+  for (int i = 0; i < MPL; ++i) {                   // all loads first
+    const int kb = min(max(lane + NT * i - HF, 0), NB - 1);
+    bv[i] = br[kb];
+    thv[i] = a.thresh[kb];
+  }
+  double g[NG_F];
+#pragma unroll
+  for (int j = 0; j < NG_F; ++j) g[j] = tb.gf[j];
+#pragma unroll
+  for (int i = 0; i < MPL; ++i) {
+    const int k = lane + NT * i, kb = k - HF;
+    if (k >= NB + 2 * HF) continue;
     float v = 0.0f;
     if (kb >= 0 && kb < NB) {
-      const bool m = br[kb] || c > (double)a.thresh[kb];
+      const bool m = bv[i] || c > (double)thv[i];
       v = (float)((m ? 1.0 : 0.0) * p + (1.0 - p));     // exact in float for p = 1 (0 / 1)
     }
     mrow[k] = v;
   }
   lds_order();
+  // lane: bins 8 lane .. 8 lane + 7 from the 40 mask values mrow[8 lane .. 8 lane + 39] (ten
+  // 16-B reads); bin 512 by lane 0.  Same summation order as the direct 33-tap sum.
   double* row = a.rows + (item * a.T + t) * NB;
-  for (int k = lane; k < NB; k += NT) {
-    double sacc = 0.0;
+  {
+    float m[8 + NG_F - 1];
+    const float4* m4 = reinterpret_cast<const float4*>(mrow + 8 * lane);
 #pragma unroll
-    for (int j = 0; j < NG_F; ++j) sacc = fma(tb.gf[j], (double)mrow[k + j], sacc);
-    row[k] = sacc;
+    for (int q = 0; q < (8 + NG_F - 1) / 4; ++q) {
+      const float4 u = m4[q];
+      m[4 * q] = u.x;
+      m[4 * q + 1] = u.y;
+      m[4 * q + 2] = u.z;
+      m[4 * q + 3] = u.w;
+    }
+    double o[8];
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      double sacc = 0.0;
+#pragma unroll
+      for (int j = 0; j < NG_F; ++j) sacc = fma(g[j], (double)m[b + j], sacc);
+      o[b] = sacc;
+    }
+#pragma unroll
+    for (int b = 0; b < 8; ++b) row[8 * lane + b] = o[b];
+    if (lane == 0) {
+      double sacc = 0.0;
+#pragma unroll
+      for (int j = 0; j < NG_F; ++j) sacc = fma(g[j], (double)mrow[512 + j], sacc);
+      row[512] = sacc;
+    }
   }
 }
 
 // ---- time smoothing of the rows x S -> inverse FFT -> windowed time-domain frame ------------------
 __global__ void __launch_bounds__(NT) nr_gate_kernel(NrArgs a) {
   __shared__ cd buf[512];
+  __shared__ double msk[NB];
   const int lane = threadIdx.x;
-  const int64_t item = blockIdx.x / a.T;
-  const int t = (int)(blockIdx.x - item * a.T);
+  const int64_t fr = frame_of_block(a);
+  if (fr < 0) return;
+  const int64_t item = fr / a.T;
+  const int t = (int)(fr - item * a.T);
   if (!reaches(a, t, 0)) return;
   const NrTables& tb = *a.tables;
   constexpr int HT = NG_T / 2;
@@ -234,20 +315,50 @@ __global__ void __launch_bounds__(NT) nr_gate_kernel(NrArgs a) {
     rows[j] = a.rows + (item * a.T + (rin[j] ? tr : 0)) * NB;
   }
   const double2* S = a.S + (item * a.T + t) * NB;
-  // gated spectrum -> Z[k] = E[k] + i O[k] of the inverse real FFT (k = 0..511)
-  for (int k = lane; k < 512; k += NT) {
-    double mk = 0.0, mr = 0.0;
+  // the time-smoothed mask of the frame, once per bin (the gate reads bins k and 512 - k); the
+  // rows' loads are all issued before the first FMA, S and the twiddles right behind them
+  double gt[NG_T];
 #pragma unroll
-    for (int j = 0; j < NG_T; ++j)
-      if (rin[j]) {
-        mk = fma(tb.gt[j], rows[j][k], mk);
-        mr = fma(tb.gt[j], rows[j][512 - k], mr);
-      }
-    const double2 s0 = S[k], s1 = S[512 - k];
+  for (int j = 0; j < NG_T; ++j) gt[j] = tb.gt[j];
+  {
+    double rv[KPL][NG_T];
+#pragma unroll
+    for (int i = 0; i < KPL; ++i) {
+      const int k = min(lane + NT * i, NB - 1);
+#pragma unroll
+      for (int j = 0; j < NG_T; ++j) rv[i][j] = rows[j][k];
+    }
+#pragma unroll
+    for (int i = 0; i < KPL; ++i) {
+      const int k = lane + NT * i;
+      double mk = 0.0;
+#pragma unroll
+      for (int j = 0; j < NG_T; ++j)
+        if (rin[j]) mk = fma(gt[j], rv[i][j], mk);
+      if (k < NB) msk[k] = mk;
+    }
+  }
+  constexpr int ZPL = 512 / NT;   // 8
+  double2 s0v[ZPL], s1v[ZPL];
+  cd wcv[ZPL];
+#pragma unroll
+  for (int i = 0; i < ZPL; ++i) {
+    const int k = lane + NT * i;
+    s0v[i] = S[k];
+    s1v[i] = S[512 - k];
+    wcv[i] = cd{tb.w1024[k][0], -tb.w1024[k][1]};                       // W1024^-k
+  }
+  lds_order();
+  // gated spectrum -> Z[k] = E[k] + i O[k] of the inverse real FFT (k = 0..511)
+#pragma unroll
+  for (int i = 0; i < ZPL; ++i) {
+    const int k = lane + NT * i;
+    const double mk = msk[k], mr = msk[512 - k];
+    const double2 s0 = s0v[i], s1 = s1v[i];
     const cd X = {s0.x * mk, s0.y * mk}, Xr = {s1.x * mr, s1.y * mr};   // X[k], X[512 - k]
     const cd e = {0.5 * (X.x + Xr.x), 0.5 * (X.y - Xr.y)};             // (X[k] + conj X[512-k]) / 2
     const cd d = {0.5 * (X.x - Xr.x), 0.5 * (X.y + Xr.y)};             // (X[k] - conj X[512-k]) / 2
-    const cd wc = {tb.w1024[k][0], -tb.w1024[k][1]};                   // W1024^-k
+    const cd wc = wcv[i];
     const cd o = cmul(d, wc);                                          // O[k]
     // conj(Z) for the forward FFT used as an inverse: Z = E + i O
     const cd Z = {e.x - o.y, e.y + o.x};
@@ -257,6 +368,7 @@ __global__ void __launch_bounds__(NT) nr_gate_kernel(NrArgs a) {
   fft512(buf, tb.w512, lane);
   // z[n] = conj(FFT(conj Z))[n] / 512 = x[2n] + i x[2n+1]; windowed frame to HBM
   double* out = a.frames + (item * a.T + t) * NFFT;
+#pragma unroll
   for (int n = lane; n < 512; n += NT) {
     const cd z = buf[n];
     const double x0 = z.x * (1.0 / 512.0), x1 = -z.y * (1.0 / 512.0);
@@ -395,8 +507,10 @@ hipError_t nr_noise_launch(const float* noise, int64_t m, const NrTables* tables
 
 hipError_t nr_gate_launch(const NrArgs& a, hipStream_t s) {
   if (a.n_items <= 0) return hipSuccess;
-  const unsigned frames = (unsigned)(a.n_items * a.T);
+  const int64_t total = a.n_items * a.T;
+  const unsigned frames = (unsigned)((total + NXCD - 1) / NXCD * NXCD);   // frame_of_block
   hipLaunchKernelGGL(nr_stft_kernel, dim3(frames), dim3(NT), 0, s, a);
+  hipLaunchKernelGGL(nr_gmax_kernel, dim3((unsigned)a.n_items), dim3(NT), 0, s, a);
   hipLaunchKernelGGL(nr_rows_kernel, dim3(frames), dim3(NT), 0, s, a);
   hipLaunchKernelGGL(nr_gate_kernel, dim3(frames), dim3(NT), 0, s, a);
   const int64_t tot = a.n_items * a.keep_len;
