@@ -869,6 +869,9 @@ int mmla_nr_reduce(mmla_ctx* c, const float* y, int64_t n_signals, int64_t strid
     a.T = T;
     a.keep0 = kNrPadding;
     a.keep_len = keep;
+    int t_hi = T - 1;
+    nr_frame_range(items.data() + i0, ni, L, T, a.keep0, a.keep_len, &a.t_lo, &t_hi);
+    a.t_n = t_hi - a.t_lo + 1;
     a.tables = c->nr_tables;
     a.thresh = c->nr_thresh;
     a.prop_decrease = 1.0;

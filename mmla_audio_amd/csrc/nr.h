@@ -31,6 +31,8 @@ struct NrArgs {
   int64_t n_items;
   int64_t L;                    // buffer length: chunk + 2 * padding
   int T;                        // STFT frames per buffer: 1 + L / 256
+  int t_lo, t_n;                // frames launched per item: every frame that is not an all-zero
+                                // window or whose mask the gate needs (host: nr_frame_range)
   int64_t keep0, keep_len;      // kept interior of every buffer
   const NrTables* tables;
   const float* thresh;          // [513] noise threshold (dB, float32)
@@ -49,3 +51,7 @@ void nr_build_tables(NrTables* t, int sr);
 hipError_t nr_noise_launch(const float* noise, int64_t m, const NrTables* tables, float* db_scratch,
                            float* fmax_scratch, float n_std, float* thresh, hipStream_t s);
 hipError_t nr_gate_launch(const NrArgs& a, hipStream_t s);
+// [t_lo, t_hi] covering, for every item, the frames whose window overlaps its signal and the frames
+// within the time-smoothing halo of the kept interior
+void nr_frame_range(const NrItem* items, int64_t n_items, int64_t L, int T, int64_t keep0,
+                    int64_t keep_len, int* t_lo, int* t_hi);

@@ -26,6 +26,8 @@
 #include "common.h"
 #include "nr.h"
 
+#include <algorithm>
+
 #include <cmath>
 #include <vector>
 
@@ -119,7 +121,7 @@ MMLA_DEV void fft512(cd* buf, const cd* tw, int lane) {
 // signal samples and the 7 smoothing rows -- meet in the same L2.  -1: past the last frame.
 constexpr int NXCD = 8;
 MMLA_DEV int64_t frame_of_block(const NrArgs& a) {
-  const int64_t total = a.n_items * a.T, per = (total + NXCD - 1) / NXCD;
+  const int64_t total = a.n_items * a.t_n, per = (total + NXCD - 1) / NXCD;
   const int64_t f = (int64_t)(blockIdx.x % NXCD) * per + blockIdx.x / NXCD;
   return f < total ? f : -1;
 }
@@ -158,8 +160,8 @@ __global__ void __launch_bounds__(NT) nr_stft_kernel(NrArgs a) {
   const int lane = threadIdx.x;
   const int64_t fr = frame_of_block(a);
   if (fr < 0) return;
-  const int64_t item = fr / a.T;
-  const int t = (int)(fr - item * a.T);
+  const int64_t item = fr / a.t_n;
+  const int t = a.t_lo + (int)(fr - item * a.t_n);
   const NrItem it = a.items[item];
   const NrTables& tb = *a.tables;
   double2* S = a.S + (item * a.T + t) * NB;
@@ -212,11 +214,12 @@ MMLA_DEV bool reaches(const NrArgs& a, int64_t t, int halo) {
   return f_lo < a.keep0 + a.keep_len && f_hi > a.keep0;
 }
 
-// ---- the item's max dB over all frames (amplitude_to_db's top_db reference) -------------------------
+// ---- the item's max dB over all frames (amplitude_to_db's top_db reference): frames outside the
+// launched range [t_lo, t_lo + t_n) are all-zero windows, whose dB (-400) no frame is below ----------
 __global__ void __launch_bounds__(NT) nr_gmax_kernel(NrArgs a) {
   const int64_t item = blockIdx.x;
   double gm = -INFINITY;
-  for (int i = threadIdx.x; i < a.T; i += NT) gm = fmax(gm, a.fmax[item * a.T + i]);
+  for (int i = a.t_lo + threadIdx.x; i < a.t_lo + a.t_n; i += NT) gm = fmax(gm, a.fmax[item * a.T + i]);
   gm = wave_max(gm);
   if (threadIdx.x == 0) a.gmax[item] = gm;
 }
@@ -227,8 +230,8 @@ __global__ void __launch_bounds__(NT) nr_rows_kernel(NrArgs a) {
   const int lane = threadIdx.x;
   const int64_t fr = frame_of_block(a);
   if (fr < 0) return;
-  const int64_t item = fr / a.T;
-  const int t = (int)(fr - item * a.T);
+  const int64_t item = fr / a.t_n;
+  const int t = a.t_lo + (int)(fr - item * a.t_n);
   if (!reaches(a, t, NG_T / 2)) return;
   const NrTables& tb = *a.tables;
   constexpr int HF = NG_F / 2;
@@ -301,8 +304,8 @@ __global__ void __launch_bounds__(NT) nr_gate_kernel(NrArgs a) {
   const int lane = threadIdx.x;
   const int64_t fr = frame_of_block(a);
   if (fr < 0) return;
-  const int64_t item = fr / a.T;
-  const int t = (int)(fr - item * a.T);
+  const int64_t item = fr / a.t_n;
+  const int t = a.t_lo + (int)(fr - item * a.t_n);
   if (!reaches(a, t, 0)) return;
   const NrTables& tb = *a.tables;
   constexpr int HT = NG_T / 2;
@@ -505,9 +508,25 @@ hipError_t nr_noise_launch(const float* noise, int64_t m, const NrTables* tables
   return hipGetLastError();
 }
 
+void nr_frame_range(const NrItem* items, int64_t n_items, int64_t L, int T, int64_t keep0,
+                    int64_t keep_len, int* t_lo, int* t_hi) {
+  // frame t reads buffer samples [HOP t - NFFT/2, HOP t + NFFT/2), reflected into [0, L)
+  const int64_t H = NG_T / 2;
+  int64_t lo = std::max<int64_t>(0, (keep0 - NFFT / 2) / HOP - H - 1);
+  int64_t hi = std::min<int64_t>(T - 1, (keep0 + keep_len + NFFT / 2) / HOP + H + 1);
+  for (int64_t i = 0; i < n_items; ++i) {
+    const int64_t s0 = std::max<int64_t>(0, -items[i].i1), s1 = std::min<int64_t>(L, items[i].n - items[i].i1);
+    if (s1 <= s0) continue;
+    lo = std::min<int64_t>(lo, s0 <= NFFT / 2 + 1 ? 0 : (s0 - NFFT / 2) / HOP - 1);
+    hi = std::max<int64_t>(hi, s1 >= L - NFFT / 2 - 1 ? T - 1 : std::min<int64_t>(T - 1, (s1 + NFFT / 2) / HOP + 1));
+  }
+  *t_lo = (int)std::max<int64_t>(0, lo);
+  *t_hi = (int)std::min<int64_t>(T - 1, hi);
+}
+
 hipError_t nr_gate_launch(const NrArgs& a, hipStream_t s) {
   if (a.n_items <= 0) return hipSuccess;
-  const int64_t total = a.n_items * a.T;
+  const int64_t total = a.n_items * a.t_n;
   const unsigned frames = (unsigned)((total + NXCD - 1) / NXCD * NXCD);   // frame_of_block
   hipLaunchKernelGGL(nr_stft_kernel, dim3(frames), dim3(NT), 0, s, a);
   hipLaunchKernelGGL(nr_gmax_kernel, dim3((unsigned)a.n_items), dim3(NT), 0, s, a);

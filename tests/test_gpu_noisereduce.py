@@ -70,3 +70,24 @@ def test_unsupported_modes_raise():
         nr.reduce_noise(y=y, sr=16000, stationary=False)
     with pytest.raises(NotImplementedError):
         nr.reduce_noise(y=y, sr=16000, stationary=True, prop_decrease=0.5)
+
+
+@pytest.mark.parametrize('n', [1, 10, 700, 1025, 5000])
+def test_short_signals(n):
+    """Signals shorter than one frame / a few frames: every window reaches the buffer's reflect
+    edges' zero padding, and the launched frame range (nr_frame_range) is small."""
+    from mmla_audio_amd import noisereduce as nr
+    noise, ys = _signals()
+    y = ys[1][:n].copy()
+    got = nr.reduce_noise(y=y, sr=16000, y_noise=noise, stationary=True)
+    _close(got, onr.reduce_noise(y, 16000, noise))
+
+
+def test_silent_signal():
+    """All-zero input: every frame is the -400 dB floor (the top_db reference of the chunk)."""
+    from mmla_audio_amd import noisereduce as nr
+    noise, _ = _signals()
+    y = np.zeros(40000, np.float32)
+    got = nr.reduce_noise(y=y, sr=16000, y_noise=noise, stationary=True)
+    want = onr.reduce_noise(y, 16000, noise)
+    assert np.array_equal(got, want.astype(np.float32))
