@@ -498,6 +498,24 @@ __global__ void __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(R
         }
     }
   } else {
+    // all of the lane's residual loads are issued before its first store: y and x are distinct
+    // buffers, but the compiler cannot know that, and a load it may not hoist above the previous
+    // store waits a full memory latency per element
+    float rsd[NTW][MT2][4];
+#pragma unroll
+    for (int nt = 0; nt < NTW; ++nt) {
+      const int n = (wn * NTW + nt) * 16 + col;
+#pragma unroll
+      for (int m = 0; m < MT2; ++m) {
+        // clamped into the image, loaded unconditionally (a static load count, no branches)
+        const int oh = min(h0 + wm * MT2 + m, a.h - 1);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int ow = min(w0 + 4 * grp + i, a.w - 1);
+          rsd[nt][m][i] = a.x[(((int64_t)clip * a.h + oh) * a.w + ow) * C + n];
+        }
+      }
+    }
 #pragma unroll
     for (int nt = 0; nt < NTW; ++nt) {
       const int n = (wn * NTW + nt) * 16 + col;
@@ -511,7 +529,7 @@ __global__ void __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(R
         for (int i = 0; i < 4; ++i) {
           if (!interior && w0 + 4 * grp + i >= a.w) continue;
           const int64_t o = (rowbase + i) * C + n;
-          a.y[o] = d1[m][nt][i] + d2[m][nt][i] * LO_INV + b + a.x[o];
+          a.y[o] = d1[m][nt][i] + d2[m][nt][i] * LO_INV + b + rsd[nt][m][i];
         }
       }
     }
