@@ -153,8 +153,32 @@ __global__ void __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(R
   const int h0 = th_i * TH, w0 = (tile - th_i * a.tiles_w) * TW;
 
   RB_MARK(0);
-  // ---- issue the halo loads (all in flight at once) ----------------------------------------------
+  // ---- per-thread parameters first: BN1 (+ stem) for the staging, BN2 / bias for the t1 re-staging
+  //      and the epilogue.  Issued here they share the halo's memory latency; issued where they are
+  //      used (after a barrier or a dependent wait) each group cost a round trip of its own --------
   const int q = tid % QPP;
+  const float4 sc4 = *reinterpret_cast<const float4*>(a.s1 + 4 * q);
+  const float4 sh4 = *reinterpret_cast<const float4*>(a.t1 + 4 * q);
+  float stw[3][4], stb[4];   // STEM: this thread's stem weights (channels 4q .. 4q+3)
+  if constexpr (STEM) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) stw[k][c] = a.wst[k * a.ldst + 4 * q + c];
+      stb[c] = a.bst[4 * q + c];
+    }
+  }
+  float ps2[NTW], pb1[NTW], pt2[NTW], pbo[NTW];   // BN2 scale / conv-1 bias / BN2 shift, out bias
+#pragma unroll
+  for (int nt = 0; nt < NTW; ++nt) {
+    const int n = (wn * NTW + nt) * 16 + col;
+    ps2[nt] = a.s2[n];
+    pb1[nt] = a.b1[n];
+    pt2[nt] = a.t2[n];
+    pbo[nt] = POOL ? a.b2[n] + a.bs[n] : a.b2[n];
+  }
+
+  // ---- issue the halo loads (all in flight at once) ----------------------------------------------
   float4 pre[MAXT];
   uint32_t valid = 0;
   {
@@ -234,20 +258,20 @@ __global__ void __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(R
     }
   }
 
+  // GEMM 1's first PF k-steps of B: in flight across the staging and its barrier
+  const int b1o = ((wn * NTW) * 16 + col) * K1PAD + 8 * grp;   // + nt * 16 * K1PAD
+  f16x8 bh[PF][NTW], bl[PF][NTW];   // ring of B fragments, PF k-steps ahead
+#pragma unroll
+  for (int s = 0; s < PF && s < KS1; ++s)
+#pragma unroll
+    for (int nt = 0; nt < NTW; ++nt) {
+      bh[s][nt] = *reinterpret_cast<const f16x8*>(a.w1h + b1o + nt * 16 * K1PAD + 32 * s);
+      bl[s][nt] = *reinterpret_cast<const f16x8*>(a.w1l + b1o + nt * 16 * K1PAD + 32 * s);
+    }
+
   RB_MARK(1);
   // ---- stage: BN1 + ELU once per element, split hi/lo; zero outside the image (conv padding) ----
-  float stw[3][4], stb[4];   // STEM: this thread's stem weights (channels 4q .. 4q+3)
-  if constexpr (STEM) {
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-#pragma unroll
-      for (int k = 0; k < 3; ++k) stw[k][c] = a.wst[k * a.ldst + 4 * q + c];
-      stb[c] = a.bst[4 * q + c];
-    }
-  }
   {
-    const float4 sc4 = *reinterpret_cast<const float4*>(a.s1 + 4 * q);
-    const float4 sh4 = *reinterpret_cast<const float4*>(a.t1 + 4 * q);
     const f32x2 sc01 = {sc4.x, sc4.y}, sc23 = {sc4.z, sc4.w};
     const f32x2 sh01 = {sh4.x, sh4.y}, sh23 = {sh4.z, sh4.w};
 #pragma unroll
@@ -321,15 +345,6 @@ __global__ void __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(R
       acc2[m][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
   {
-    const int b1o = ((wn * NTW) * 16 + col) * K1PAD + 8 * grp;   // + nt * 16 * K1PAD
-    f16x8 bh[PF][NTW], bl[PF][NTW];   // ring of B fragments, PF k-steps ahead
-#pragma unroll
-    for (int s = 0; s < PF && s < KS1; ++s)
-#pragma unroll
-      for (int nt = 0; nt < NTW; ++nt) {
-        bh[s][nt] = *reinterpret_cast<const f16x8*>(a.w1h + b1o + nt * 16 * K1PAD + 32 * s);
-        bl[s][nt] = *reinterpret_cast<const f16x8*>(a.w1l + b1o + nt * 16 * K1PAD + 32 * s);
-      }
     const _Float16* ahb = smem + (wm * MT1 * XC + col) * XPS;   // + m * XC * XPS (immediate)
     const _Float16* alb = ahb + G::XLO;
 #pragma unroll
@@ -384,8 +399,8 @@ __global__ void __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(R
 #pragma unroll
     for (int nt = 0; nt < NTW; ++nt) {
       const int n = (wn * NTW + nt) * 16 + col;
-      const float s2 = a.s2[n];
-      const float c2 = fmaf(a.b1[n], s2, a.t2[n]);
+      const float s2 = ps2[nt];
+      const float c2 = fmaf(pb1[nt], s2, pt2[nt]);
       const f32x2 s2v = {s2, s2}, s2l = {s2 * LO_INV, s2 * LO_INV}, c2v = {c2, c2};
 #pragma unroll
       for (int m = 0; m < MT1; ++m) {
@@ -475,7 +490,7 @@ __global__ void __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(R
 #pragma unroll
     for (int nt = 0; nt < NTW; ++nt) {
       const int n = (wn * NTW + nt) * 16 + col;
-      const float b = a.b2[n] + a.bs[n];
+      const float b = pbo[nt];
 #pragma unroll
       for (int j = 0; j < MSC; ++j)
 #pragma unroll
@@ -519,7 +534,7 @@ __global__ void __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(R
 #pragma unroll
     for (int nt = 0; nt < NTW; ++nt) {
       const int n = (wn * NTW + nt) * 16 + col;
-      const float b = a.b2[n];
+      const float b = pbo[nt];
 #pragma unroll
       for (int m = 0; m < MT2; ++m) {
         const int oh = h0 + wm * MT2 + m;
