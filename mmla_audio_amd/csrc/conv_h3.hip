@@ -64,6 +64,10 @@ constexpr int tile_px() { return BN == 64 && TW > 1 && !(KH == 3 && TW == 16) ? 
 // LIN_SLOTS, which stays zero.
 constexpr int LIN_SLOTS = 11, LIN_WP = 21;
 
+// register estimate (accumulators + staged halo + one tap of B) up to which tap 0's B fragments are
+// loaded before the staging instead of after its barrier (above it the variants spilled)
+constexpr int EARLY_B_VGPRS = 168;
+
 // V4: channels loaded as float4 (cin % 4 == 0); else per element (the SI stem, cin = 39).
 // PIN (Conv1D): the input rows are MaxPool1D(2, 'same') of x, taken while staging (SI pool units)
 template <int KH, int KW, int CK, int BN, int TW, int PRO, int EPI, bool POOL, bool V4 = true,
@@ -86,6 +90,9 @@ __global__ void __launch_bounds__(NT, 2) conv_h3_kernel(ConvH3Args a) {
   constexpr int NPIX = HP * WP;
   constexpr int NSTG = LIN ? LIN_SLOTS * LIN_WP : NPIX;   // staged pixels (upper bound)
   constexpr int QPP = CK / 4;             // float4 per staged pixel
+  constexpr int MAXT = (NSTG * QPP + NT - 1) / NT;     // staged float4 per thread and chunk
+  // registers allow the early loads (tap 0's B, prologue and epilogue parameters): EARLY_B_VGPRS
+  constexpr bool EARLY_B = MT * NTL * 32 + MAXT * 4 + NTL * KS * 8 <= EARLY_B_VGPRS;
   __shared__ __attribute__((aligned(16))) _Float16 lds_hi[NPIX * LDP];
   __shared__ __attribute__((aligned(16))) _Float16 lds_lo[NPIX * LDP];
 
@@ -157,6 +164,13 @@ __global__ void __launch_bounds__(NT, 2) conv_h3_kernel(ConvH3Args a) {
     wlp[nt] = a.wl + (size_t)co * a.cin_pad + koff;
   }
   const size_t tap_stride = (size_t)a.cout_pad * a.cin_pad;
+  // the epilogue's bias, loaded now: after the MFMA loop it cost a memory round trip of its own
+  float bias_r[NTL];
+#pragma unroll
+  for (int nt = 0; nt < NTL; ++nt) {
+    const int co = n0 + (wn * NTL + nt) * 32 + (lane & 31);
+    if (EARLY_B) bias_r[nt] = co < a.cout ? a.bias[co] : 0.0f;
+  }
   const float* xclip = a.x + clip * HH * a.w * a.cin;
 
   const int nchunks = a.cin_pad / CK;
@@ -166,8 +180,20 @@ __global__ void __launch_bounds__(NT, 2) conv_h3_kernel(ConvH3Args a) {
     // ---- stage the input halo of this channel chunk: prologue once per element, split hi/lo ----
     // all of this thread's halo loads are issued before the first is consumed (one HBM latency
     // per chunk, not one per element group)
-    constexpr int MAXT = (NSTG * QPP + NT - 1) / NT;
     const int nstg = LIN ? LIN_SLOTS * wpad : NPIX;
+    // this thread's channel quad is the same for every task (NT % QPP == 0): its prologue scale /
+    // shift are loaded once, ahead of the halo, instead of once per task behind it
+    // (the register-tight variants, !EARLY_B below, load them after the halo instead)
+    static_assert(NT % QPP == 0, "a thread's channel quad is fixed");
+    float4 psc = make_float4(0.f, 0.f, 0.f, 0.f), psh = psc;
+    auto load_pro = [&]() {
+      const int ci = ci0 + (tid % QPP) * 4;
+      if (PRO != PRO_NONE && ci < a.cin) {
+        psc = *reinterpret_cast<const float4*>(a.scale + ci);
+        psh = *reinterpret_cast<const float4*>(a.shift + ci);
+      }
+    };
+    if constexpr (EARLY_B) load_pro();
     float4 pre[MAXT];
     uint32_t valid = 0;
 #pragma unroll
@@ -203,17 +229,30 @@ __global__ void __launch_bounds__(NT, 2) conv_h3_kernel(ConvH3Args a) {
         }
       }
     }
+    // tap 0's B fragments: issued here they are in flight across the staging and its barrier --
+    // where the registers allow it (accumulators + halo + fragments within EARLY_B_VGPRS; the
+    // variants above it spill), else after the barrier
+    f16x8 bh[NTL][KS], bl[NTL][KS];
+    auto load_b0 = [&]() {
+#pragma unroll
+      for (int nt = 0; nt < NTL; ++nt)
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+          bh[nt][s] = *reinterpret_cast<const f16x8*>(whp[nt] + ci0 + 16 * s);
+          bl[nt][s] = *reinterpret_cast<const f16x8*>(wlp[nt] + ci0 + 16 * s);
+        }
+    };
+    if constexpr (EARLY_B) load_b0();
+    else load_pro();
 #pragma unroll
     for (int j = 0; j < MAXT; ++j) {
       const int task = tid + j * NT;
       if (task >= nstg * QPP) continue;
       const int px = task / QPP, q = task % QPP;
-      const int ci = ci0 + q * 4;
       float4 v = pre[j];
       if constexpr (PRO != PRO_NONE) {
         if (valid & (1u << j)) {
-          const float4 sc = *reinterpret_cast<const float4*>(a.scale + ci);
-          const float4 sh = *reinterpret_cast<const float4*>(a.shift + ci);
+          const float4 sc = psc, sh = psh;
           v.x = pro_fn<PRO>(v.x, sc.x, sh.x);
           v.y = pro_fn<PRO>(v.y, sc.y, sh.y);
           v.z = pro_fn<PRO>(v.z, sc.z, sh.z);
@@ -235,14 +274,7 @@ __global__ void __launch_bounds__(NT, 2) conv_h3_kernel(ConvH3Args a) {
     __syncthreads();
 
     // ---- all taps of this chunk ------------------------------------------------------------------
-    f16x8 bh[NTL][KS], bl[NTL][KS];
-#pragma unroll
-    for (int nt = 0; nt < NTL; ++nt)
-#pragma unroll
-      for (int s = 0; s < KS; ++s) {
-        bh[nt][s] = *reinterpret_cast<const f16x8*>(whp[nt] + ci0 + 16 * s);
-        bl[nt][s] = *reinterpret_cast<const f16x8*>(wlp[nt] + ci0 + 16 * s);
-      }
+    if constexpr (!EARLY_B) load_b0();
 #pragma unroll
     for (int tap = 0; tap < TAPS; ++tap) {
       constexpr int dummy = 0;
@@ -332,7 +364,7 @@ __global__ void __launch_bounds__(NT, 2) conv_h3_kernel(ConvH3Args a) {
   for (int nt = 0; nt < NTL; ++nt) {
     const int co = n0 + (wn * NTL + nt) * 32 + (lane & 31);
     if (co >= a.cout) continue;
-    const float b = a.bias[co];
+    const float b = EARLY_B ? bias_r[nt] : a.bias[co];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
       float v[16];
