@@ -4,6 +4,7 @@
 
 #include <cmath>
 #include <cstdarg>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -101,6 +102,7 @@ struct mmla_ctx {
   std::vector<void*> od_allocs, si_allocs;
   std::vector<void*> ws;
   std::vector<size_t> ws_size;
+  std::vector<size_t> ws_guard;   // MMLA_WS_GUARD: guard bytes before and after each slot (0 = none)
   int64_t od_mb = kOdMicrobatch, si_mb = kSiMicrobatch;
   int precision = MMLA_PREC_F16X3;
   NrTables* nr_tables = nullptr;   // noise gate (nr.hip): tables + the noise profile's threshold
@@ -185,25 +187,56 @@ int prof_collect(mmla_ctx* c) {
   } while (0)
 
 // growable device workspace slots
+// Debug aid: with MMLA_WS_GUARD=1 in the environment each slot allocated from then on is framed by
+// 4 MiB guard bands filled with kGuardByte, and finish() fails the call if a kernel wrote into one
+// (out-of-bounds stores that would otherwise land silently in a neighbouring allocation).
+constexpr size_t kGuardBytes = 4u << 20;
+constexpr int kGuardByte = 0xA5;
+
 int ws_get(mmla_ctx* c, int slot, size_t bytes, void** out) {
   if ((int)c->ws.size() <= slot) {
     c->ws.resize(slot + 1, nullptr);
     c->ws_size.resize(slot + 1, 0);
+    c->ws_guard.resize(slot + 1, 0);
   }
   if (c->ws_size[slot] < bytes) {
     if (c->ws[slot]) {
       HIPCHK(c, hipStreamSynchronize(c->stream));
-      HIPCHK(c, hipFree(c->ws[slot]));
+      HIPCHK(c, hipFree(static_cast<char*>(c->ws[slot]) - c->ws_guard[slot]));
       c->ws[slot] = nullptr;
       c->ws_size[slot] = 0;
     }
+    const char* ge = std::getenv("MMLA_WS_GUARD");
+    const size_t guard = ge && ge[0] == '1' ? kGuardBytes : 0;
     void* p = nullptr;
-    if (hipMalloc(&p, bytes) != hipSuccess)
+    if (hipMalloc(&p, bytes + 2 * guard) != hipSuccess)
       return fail(c, MMLA_E_OOM, "hipMalloc(%zu) failed for workspace slot %d", bytes, slot);
-    c->ws[slot] = p;
+    if (guard) {
+      HIPCHK(c, hipMemset(p, kGuardByte, guard));
+      HIPCHK(c, hipMemset(static_cast<char*>(p) + guard + bytes, kGuardByte, guard));
+    }
+    c->ws[slot] = static_cast<char*>(p) + guard;
     c->ws_size[slot] = bytes;
+    c->ws_guard[slot] = guard;
   }
   *out = c->ws[slot];
+  return MMLA_OK;
+}
+
+int ws_check_guards(mmla_ctx* c) {
+  std::vector<unsigned char> h(kGuardBytes);
+  for (size_t slot = 0; slot < c->ws.size(); ++slot) {
+    const size_t g = c->ws_guard[slot];
+    if (!c->ws[slot] || !g) continue;
+    for (int side = 0; side < 2; ++side) {
+      const char* d = static_cast<const char*>(c->ws[slot]) + (side ? c->ws_size[slot] : -(ptrdiff_t)g);
+      HIPCHK(c, hipMemcpy(h.data(), d, g, hipMemcpyDeviceToHost));
+      for (size_t i = 0; i < g; ++i)
+        if (h[i] != kGuardByte)
+          return fail(c, MMLA_E_HIP, "workspace slot %zu: %s guard overwritten at byte %zu", slot,
+                      side ? "trailing" : "leading", side ? i : g - i);
+    }
+  }
   return MMLA_OK;
 }
 
@@ -399,7 +432,10 @@ int copy_back(mmla_ctx* c, T* user, int64_t off, const T* d, size_t count, bool 
 
 int finish(mmla_ctx* c, bool dev) {
   HIPCHK(c, hipGetLastError());
-  if (!dev) HIPCHK(c, hipStreamSynchronize(c->stream));
+  bool guarded = false;
+  for (size_t g : c->ws_guard) guarded |= g != 0;
+  if (!dev || guarded) HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (guarded) return ws_check_guards(c);
   return MMLA_OK;
 }
 
@@ -758,8 +794,8 @@ int mmla_destroy(mmla_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   free_allocs(c->od_allocs);
   free_allocs(c->si_allocs);
-  for (void* p : c->ws)
-    if (p) (void)hipFree(p);
+  for (size_t i = 0; i < c->ws.size(); ++i)
+    if (c->ws[i]) (void)hipFree(static_cast<char*>(c->ws[i]) - c->ws_guard[i]);
   if (c->od_tables) (void)hipFree(c->od_tables);
   if (c->si_tables) (void)hipFree(c->si_tables);
   if (c->nr_tables) (void)hipFree(c->nr_tables);
