@@ -56,6 +56,8 @@ def parse():
                     choices=['od_pipeline', 'si_pipeline', 'od_features', 'noise_gate'])
     ap.add_argument('--clips', type=int, default=None, help='clips per GPU')
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--microbatch', type=int, default=0,
+                    help='clips per internal micro-batch (0 = the library default)')
     ap.add_argument('--cpu-seconds', type=float, default=15.0)
     return ap.parse_args()
 
@@ -162,6 +164,9 @@ def main():
     from mmla_audio_amd.synthetic import make_clips
 
     ctx = _lib.Context(local)
+    if args.microbatch:
+        ctx.set_microbatch(args.microbatch if args.workload == 'od_pipeline' else 0,
+                           args.microbatch if args.workload == 'si_pipeline' else 0)
     stream = torch.cuda.current_stream()
     ctx.set_stream(stream.cuda_stream)
     wl = args.workload
