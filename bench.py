@@ -1,8 +1,12 @@
 #!/usr/bin/env python3
 """Benchmark: audio clips/s (MFCC -> logits) on 1..8 MI355X, one process per GPU.
 
-  python bench.py [--gpus N --steps K --warmup W --workload od_pipeline|si_pipeline|od_features]
-  torchrun --nproc-per-node N ... bench.py --gpus N   (RCCL all-gather of the logits per step)
+  python bench.py [--gpus N --steps K --warmup W --workload od_pipeline|si_pipeline|od_features|noise_gate]
+
+With --gpus N > 1 and no torchrun environment, bench.py starts
+`python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py` as a child
+process before anything touches a GPU and exits with its code; under torchrun (WORLD_SIZE set) each
+rank drives its LOCAL_RANK GPU and the per-step probabilities are all-gathered over RCCL.
 
 A step = one pass of the hot path over one batch of synthetic clips already resident in HBM:
   od_pipeline (default, BASELINE config 3): 65 536 x 2.5 s clips / GPU, fused log-mel+ZCR front-end
@@ -10,11 +14,14 @@ A step = one pass of the hot path over one batch of synthetic clips already resi
       at N GPUs the per-shard probabilities are all-gathered over RCCL (config 5 at N = 8).
   si_pipeline (config 4): 65 536 x 1.5 s clips / GPU, MFCC+delta+delta-delta -> SI-NET, K = 630.
   od_features (config 2): the front-end kernel alone, 4 096 x 2.5 s clips / GPU.
-Prints ONE JSON line (rank 0) with roofline + cpu_baseline objects (see DESIGN.md).
+  noise_gate: the stationary noise gate on 4 096 x 2.5 s clips / GPU.
+Prints ONE JSON line (rank 0) with roofline + cpu_baseline objects (see DESIGN.md section 5).
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -31,9 +38,11 @@ F16_MFMA_PEAK_TFS = 2516.6   # f16 MFMA dense (~2.5 PF spec, no sparsity)
 # 3xFP16 spends three f16 MFMA products per f32 MAC: its f32-equivalent ceiling is F16 / 3
 F16X3_PEAK_TFS = F16_MFMA_PEAK_TFS / 3
 OD_FE_BYTES = 48000 + 128 * 151 * 4 + 151 * 4          # 125 916 B/clip
+HBM_STAGES = ('od_fe', 'si_fe', 'nr')
+PREC_F32, PREC_F16X3 = 0, 1
 
 
-def pmc_traffic(workload, stage, clips):
+def pmc_traffic(workload, stage, clips_per_launch):
     """HBM bytes per launch of `stage` from the committed PMC capture of this workload
     (tools/gpu/pmc_traffic.sh -> profiles/pmc_traffic_<workload>.json), scaled to this run's clips
     per launch; None when no capture exists."""
@@ -42,7 +51,7 @@ def pmc_traffic(workload, stage, clips):
         d = json.load(open(path))
         st = d['stages'][stage]
         per_clip = st['traffic_bytes_per_launch'] / d['clips_per_launch'][stage]
-        return per_clip * min(clips, d['clips_per_launch'][stage]), os.path.relpath(path, REPO)
+        return per_clip * clips_per_launch, os.path.relpath(path, REPO)
     except (OSError, KeyError, ValueError, ZeroDivisionError):
         return None, None
 
@@ -56,23 +65,36 @@ def parse():
                     choices=['od_pipeline', 'si_pipeline', 'od_features', 'noise_gate'])
     ap.add_argument('--clips', type=int, default=None, help='clips per GPU')
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--no-f32', action='store_true', help='skip the exact-f32 precision leg')
+    ap.add_argument('--no-parity', action='store_true', help='skip the oracle parity sample')
     ap.add_argument('--microbatch', type=int, default=0,
                     help='clips per internal micro-batch (0 = the library default)')
-    ap.add_argument('--cpu-seconds', type=float, default=15.0)
+    ap.add_argument('--cpu-seconds', type=float, default=20.0)
     return ap.parse_args()
+
+
+def launch_ranks(args):
+    """--gpus N outside torchrun: run N ranks under torch.distributed.run as a child process
+    (no GPU has been touched in this process) and return its exit code."""
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1',
+           f'--nproc-per-node={args.gpus}', '--master-addr', '127.0.0.1', '--master-port', str(port),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd, env=dict(os.environ, MASTER_ADDR='127.0.0.1'))
 
 
 def dist_setup():
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
+    torch.cuda.set_device(local)
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
-        torch.cuda.set_device(local)
         dist.init_process_group('nccl', device_id=torch.device('cuda', local))
-    else:
-        torch.cuda.set_device(local)
     return world, rank, local
 
 
@@ -91,104 +113,139 @@ def max_over_ranks(x, world):
     return float(t.item())
 
 
-def cpu_baseline_od(pcm_sample, gpu_norm, gpu_probs, W, budget_s):
-    """Oracle (numpy) FE + OD-NET on a bounded sample of the same clips, on the host cores."""
-    from oracle import nets, od_fe
-    threads = int(os.environ.get('OMP_NUM_THREADS', os.cpu_count() or 1))
-    n_done = 0
-    err_norm = 0.0
-    err_prob = 0.0
-    t0 = time.perf_counter()
-    for i in range(len(pcm_sample)):
-        f = od_fe.od_features(pcm_sample[i])
-        p = nets.od_forward(f['png_rgb'][None].astype(np.float32), W, dtype=np.float32)
-        ok = ~np.isnan(f['norm'])
-        if ok.any():
-            err_norm = max(err_norm, float(np.abs(gpu_norm[i][ok] - f['norm'][ok]).max()))
-        err_prob = max(err_prob, float(np.abs(gpu_probs[i] - p[0]).max()))
-        n_done += 1
-        if time.perf_counter() - t0 > budget_s:
-            break
-    dt = time.perf_counter() - t0
-    return {'value': n_done / dt, 'unit': 'clips/s', 'cores': threads, 'kind': 'port',
-            'sample': f'{n_done} x 2.5 s synthetic clips, batch 1 (record_on_pc.py loop shape): '
-                      f'numpy librosa-0.8 restatement + numpy float32 OD-NET (BLAS threads={threads})'}, \
-        err_norm, err_prob
+def rank_devices(world, rank, local):
+    p = torch.cuda.get_device_properties(local)
+    me = {'rank': rank, 'local_rank': local, 'device': local, 'name': p.name,
+          'pci_bus_id': getattr(p, 'pci_bus_id', None), 'pci_device_id': getattr(p, 'pci_device_id', None),
+          'host': socket.gethostname()}
+    if world == 1:
+        return [me]
+    import torch.distributed as dist
+    out = [None] * world
+    dist.all_gather_object(out, me)
+    return out
 
 
-def cpu_baseline_nr(y_sample, noise, gpu_out, budget_s):
-    """Oracle (numpy/scipy) noisereduce-2.0 stationary gate on a bounded sample of the clips."""
-    from oracle import noisereduce as onr
-    threads = int(os.environ.get('OMP_NUM_THREADS', os.cpu_count() or 1))
-    n_done, err = 0, 0.0
-    t0 = time.perf_counter()
-    for i in range(len(y_sample)):
-        w = onr.reduce_noise(y_sample[i], 16000, noise)
-        err = max(err, float(np.abs(gpu_out[i] - w).max()))
-        n_done += 1
-        if time.perf_counter() - t0 > budget_s:
-            break
-    dt = time.perf_counter() - t0
-    return {'value': n_done / dt, 'unit': 'clips/s', 'cores': threads, 'kind': 'port',
-            'sample': f'{n_done} x 2.5 s synthetic clips, one call each (record_on_pc.py shape): numpy '
-                      f'librosa-0.8 stft/istft + scipy fftconvolve restatement of noisereduce 2.0 '
-                      f'(BLAS threads={threads})'}, err
+def roofline(prof, wl, clips_per_launch, prec):
+    """dominant stage: algorithmic work per launch / average launch time (HIP events)"""
+    stage = max(prof, key=lambda s: prof[s][0])
+    ms, launches, work = prof[stage]
+    if stage in HBM_STAGES:
+        achieved = work / (ms * 1e-3) / 1e9
+        roof = {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                'frac': achieved / HBM_PEAK_GBS, 'traffic': None}
+    else:
+        achieved = work / (ms * 1e-3) / 1e12
+        f16 = stage in ('conv', 'lstm') and prec == PREC_F16X3
+        peak = F16X3_PEAK_TFS if f16 else F32_MFMA_PEAK_TFS
+        roof = {'bound': 'mfma', 'achieved': achieved, 'peak': peak, 'unit': 'TFLOP/s',
+                'frac': achieved / peak, 'traffic': None,
+                'arith': '3xFP16 on f16 MFMA (peak = f16 dense / 3)' if f16 else 'f32 MFMA'}
+    roof.update({'kernel': stage, 'launches': launches, 'avg_launch_ms': ms / max(launches, 1),
+                 'work_per_launch': work / max(launches, 1)})
+    roof['traffic'], roof['traffic_source'] = pmc_traffic(wl, stage, clips_per_launch)
+    return roof
 
 
-def cpu_baseline_si(pcm_sample, gpu_feat, gpu_probs, W, budget_s):
-    from oracle import nets, si_fe
-    threads = int(os.environ.get('OMP_NUM_THREADS', os.cpu_count() or 1))
-    n_done = 0
-    err_feat = 0.0
-    err_prob = 0.0
-    t0 = time.perf_counter()
-    for i in range(len(pcm_sample)):
-        x = si_fe.input_feature_gen(pcm_sample[i])
-        p = nets.si_forward(x.astype(np.float32), W, dtype=np.float32)
-        err_feat = max(err_feat, float(np.abs(gpu_feat[i] - x[0]).max()))
-        err_prob = max(err_prob, float(np.abs(gpu_probs[i] - p[0]).max()))
-        n_done += 1
-        if time.perf_counter() - t0 > budget_s:
-            break
-    dt = time.perf_counter() - t0
-    return {'value': n_done / dt, 'unit': 'clips/s', 'cores': threads, 'kind': 'port',
-            'sample': f'{n_done} x 1.5 s synthetic clips, batch 1: numpy python_speech_features-0.6 '
-                      f'restatement + numpy float32 SI-NET (BLAS threads={threads})'}, \
-        err_feat, err_prob
+def stage_table(prof):
+    return {s: {'ms': round(v[0], 3), 'launches': v[1],
+                ('GB/s' if s in HBM_STAGES else 'TFLOP/s'):
+                    round(v[2] / (v[0] * 1e-3) / (1e9 if s in HBM_STAGES else 1e12), 3) if v[0] > 0 else 0.0}
+            for s, v in prof.items() if v[1]}
+
+
+def sample_indices(n, mb, k, seed=20261015):
+    """first and last clip of every micro-batch + k seeded random clips"""
+    idx = set()
+    for c0 in range(0, n, mb):
+        idx.update((c0, min(c0 + mb, n) - 1))
+    idx.update(np.random.default_rng(seed).choice(n, min(k, n), replace=False).tolist())
+    return sorted(idx)
+
+
+def parity_sample(ctx, wl, pcm, probs, argmax, W, mb, clip_len, k=24):
+    """oracle (float64) vs the timed run's outputs on clips spread across the whole batch"""
+    from oracle import od_fe, si_fe
+    from oracle.nets_torch import Nets
+    n = pcm.shape[0]
+    idx = sample_indices(n, mb, k)
+    sub = pcm[idx].contiguous()
+    host = sub.cpu().numpy()
+    out = {'sample_clips': len(idx), 'sample': 'first + last clip of every micro-batch and '
+           f'{min(k, n)} seeded random clips of the {n}-clip batch; float64 oracle'}
+    if wl in ('od_pipeline', 'od_features'):
+        norm = torch.empty((len(idx), 128, 151), dtype=torch.float32, device='cuda')
+        ctx.od_features_dev(sub.data_ptr(), len(idx), clip_len, clip_len, norm=norm.data_ptr())
+        torch.cuda.synchronize()
+        norm = norm.cpu().numpy()
+        feats = [od_fe.od_features(host[j]) for j in range(len(idx))]
+        err = 0.0
+        for j, f in enumerate(feats):
+            ok = ~np.isnan(f['norm'])
+            if ok.any():
+                err = max(err, float(np.abs(norm[j][ok] - f['norm'][ok]).max()))
+        out['od_norm_logmel_max_abs_err'] = err
+        if wl == 'od_pipeline':
+            ref = Nets(W).od_forward(np.stack([f['png_rgb'] for f in feats]).astype(np.float32))
+    else:
+        feat = torch.empty((len(idx), 256, 39), dtype=torch.float32, device='cuda')
+        ctx.si_features_dev(sub.data_ptr(), len(idx), clip_len, clip_len, feat.data_ptr())
+        torch.cuda.synchronize()
+        xs = np.stack([si_fe.input_feature_gen(host[j])[0] for j in range(len(idx))])
+        out['si_feature_max_abs_err'] = float(np.abs(feat.cpu().numpy() - xs).max())
+        ref = Nets(W).si_forward(xs.astype(np.float32))
+    if wl in ('od_pipeline', 'si_pipeline'):
+        gp = probs[idx].cpu().numpy()
+        ga = argmax[idx].cpu().numpy()
+        srt = np.sort(ref, axis=1)
+        tie = srt[:, -1] - srt[:, -2] < 1e-4
+        agree = ga == np.argmax(ref, axis=1)
+        out.update({'prob_max_abs_err': float(np.abs(gp - ref).max()),
+                    'argmax_agree': int(agree.sum()), 'argmax_disagree_non_tie': int((~agree & ~tie).sum()),
+                    'near_ties': int(tie.sum())})
+    return out
 
 
 def main():
     args = parse()
+    world_env = int(os.environ.get('WORLD_SIZE', '1'))
+    if args.gpus > 1 and 'WORLD_SIZE' not in os.environ:
+        sys.exit(launch_ranks(args))
+    if world_env != args.gpus:
+        print(f'bench.py: --gpus {args.gpus} but WORLD_SIZE={world_env}: measuring {world_env} '
+              'rank(s)', file=sys.stderr)
+    rank = int(os.environ.get('RANK', '0'))
+    wl = args.workload
+
+    # CPU baseline first, before this process touches a GPU (child processes, pinned cores)
+    cpu = None
+    if rank == 0 and world_env == 1 and not args.no_cpu_baseline:
+        from oracle import cpu_baseline
+        cpu = cpu_baseline.run_modes(wl, args.cpu_seconds)
+
     world, rank, local = dist_setup()
     from mmla_audio_amd import _lib, weights
+    from mmla_audio_amd.distributed import gather_logits
     from mmla_audio_amd.synthetic import make_clips
 
     ctx = _lib.Context(local)
     if args.microbatch:
-        ctx.set_microbatch(args.microbatch if args.workload == 'od_pipeline' else 0,
-                           args.microbatch if args.workload == 'si_pipeline' else 0)
+        ctx.set_microbatch(args.microbatch if wl == 'od_pipeline' else 0,
+                           args.microbatch if wl == 'si_pipeline' else 0)
     stream = torch.cuda.current_stream()
     ctx.set_stream(stream.cuda_stream)
-    wl = args.workload
-    if wl == 'od_features':
-        clips = args.clips or 4096
-        clip_len = 40000
-    elif wl == 'noise_gate':
-        clips = args.clips or 4096
-        clip_len = 40000
-    elif wl == 'si_pipeline':
-        clips = args.clips or 65536
-        clip_len = 24000
-    else:
-        clips = args.clips or 65536
-        clip_len = 40000
+    clips = args.clips or (65536 if wl in ('od_pipeline', 'si_pipeline') else 4096)
+    clip_len = 24000 if wl == 'si_pipeline' else 40000
 
-    W_od = weights.synthetic(weights.OD, seed=0)
-    W_si = weights.synthetic(weights.SI, seed=0, n_classes=630)
+    W = None
     if wl == 'od_pipeline':
-        ctx.load_weights(weights.OD, weights.pack(weights.OD, W_od), 2)
+        W = weights.synthetic(weights.OD, seed=0)
+        ctx.load_weights(weights.OD, weights.pack(weights.OD, W), 2)
     if wl == 'si_pipeline':
-        ctx.load_weights(weights.SI, weights.pack(weights.SI, W_si, 630), 630, _lib.HEAD_SOFTMAX)
+        W = weights.synthetic(weights.SI, seed=0, n_classes=630)
+        ctx.load_weights(weights.SI, weights.pack(weights.SI, W, 630), 630, _lib.HEAD_SOFTMAX)
+    mb_od, mb_si = ctx.get_microbatch()
+    mb = {'od_pipeline': mb_od, 'si_pipeline': mb_si}.get(wl, clips)
 
     pcm = make_clips(clips, clip_len, start_index=rank * clips)
     if wl == 'noise_gate':   # float32 audio as librosa.load gives it, and a 10 s ambient-noise clip
@@ -205,7 +262,8 @@ def main():
     argmax = torch.empty(clips, dtype=torch.int32, device='cuda')
     norm = torch.empty((clips, 128, 151), dtype=torch.float32, device='cuda') if wl == 'od_features' else None
     zcr = torch.empty((clips, 151), dtype=torch.float32, device='cuda') if wl == 'od_features' else None
-    gathered = torch.empty((world * clips, K), dtype=torch.float32, device='cuda') if world > 1 else None
+    pipeline = wl in ('od_pipeline', 'si_pipeline')
+    gathered = torch.empty((world * clips, K), dtype=torch.float32, device='cuda') if pipeline else None
 
     def step():
         if wl == 'od_pipeline':
@@ -219,51 +277,53 @@ def main():
         else:
             ctx.od_features_dev(pcm.data_ptr(), clips, clip_len, clip_len, norm=norm.data_ptr(),
                                 zcr=zcr.data_ptr())
-        if world > 1 and wl not in ('od_features', 'noise_gate'):
-            import torch.distributed as dist
-            dist.all_gather_into_tensor(gathered, probs)   # RCCL over xGMI: logits to every rank
+        if pipeline and world > 1:   # every rank ends the step with the whole batch's probabilities
+            gather_logits(probs, n_total=world * clips, out=gathered)
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    ctx.profile_read(reset=True)
-    ctx.profile_enable(True)
-    barrier(world)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    barrier(world)
-    dt = time.perf_counter() - t0
-    ctx.profile_enable(False)
-    prof = ctx.profile_read(reset=True)
-    dt = max_over_ranks(dt, world)
+    def timed(steps, warmup):
+        for _ in range(warmup):
+            step()
+        torch.cuda.synchronize()
+        ctx.profile_read(reset=True)
+        ctx.profile_enable(True)
+        barrier(world)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        torch.cuda.synchronize()
+        barrier(world)
+        dt = time.perf_counter() - t0
+        ctx.profile_enable(False)
+        return max_over_ranks(dt, world), ctx.profile_read(reset=True)
+
+    dt, prof = timed(args.steps, args.warmup)
     value = world * clips * args.steps / dt
+    roof = roofline(prof, wl, mb, PREC_F16X3)
+    stages = stage_table(prof)
+    range_ok = True
+    try:
+        ctx.range_check()
+    except _lib.MmlaError:
+        range_ok = False
 
-    # dominant kernel and its roofline (algorithmic work / device time from HIP events)
-    stage = max(prof, key=lambda s: prof[s][0])
-    ms, launches, work = prof[stage]
-    if stage in ('od_fe', 'si_fe', 'nr'):
-        achieved = work / (ms * 1e-3) / 1e9
-        roof = {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-                'frac': achieved / HBM_PEAK_GBS, 'traffic': None}
-    else:
-        achieved = work / (ms * 1e-3) / 1e12
-        peak = F16X3_PEAK_TFS if stage == 'conv' else F32_MFMA_PEAK_TFS
-        roof = {'bound': 'mfma', 'achieved': achieved, 'peak': peak, 'unit': 'TFLOP/s',
-                'frac': achieved / peak, 'traffic': None,
-                'arith': '3xFP16 on f16 MFMA (peak = f16 dense / 3)' if stage == 'conv' else 'f32 MFMA'}
-    roof.update({'kernel': stage, 'launches': launches, 'avg_launch_ms': ms / max(launches, 1),
-                 'work_per_launch': work / max(launches, 1)})
-    roof['traffic'], roof['traffic_source'] = pmc_traffic(wl, stage, clips)
-    stages = {s: {'ms': round(v[0], 3), 'launches': v[1],
-                  ('GB/s' if s in ('od_fe', 'si_fe', 'nr') else 'TFLOP/s'):
-                      round(v[2] / (v[0] * 1e-3) / (1e9 if s in ('od_fe', 'si_fe', 'nr') else 1e12), 3)
-                      if v[0] > 0 else 0.0}
-              for s, v in prof.items() if v[1]}
+    # the exact-f32 arithmetic on the same batch (N = 1): value and roofline beside the 3xFP16 one,
+    # and how many argmax labels the two arithmetics disagree on
+    f32 = None
+    if pipeline and world == 1 and not args.no_f32:
+        am16 = argmax.clone()
+        ctx.set_precision(PREC_F32)
+        steps32 = max(1, min(args.steps, 2))
+        dt32, prof32 = timed(steps32, 1)
+        ctx.set_precision(PREC_F16X3)
+        f32 = {'value': clips * steps32 / dt32, 'ms_per_step': dt32 / steps32 * 1e3, 'steps': steps32,
+               'dtype': 'f32' if wl == 'od_pipeline' else 'f64+f32',
+               'roofline': roofline(prof32, wl + '_f32', mb, PREC_F32), 'stages': stage_table(prof32),
+               'argmax_differs_from_f16x3': int((argmax != am16).sum().item())}
+        step()   # leave the 3xFP16 outputs in probs / argmax for the parity sample
+        torch.cuda.synchronize()
 
-    # front-end roofline on the same clips (config 2 measurement) for the pipeline workloads
+    # front-end roofline on the same clips (config 2 measurement) for the OD pipeline
     fe = None
     if wl == 'od_pipeline' and rank == 0:
         n_fe = min(clips, 4096)
@@ -282,35 +342,24 @@ def main():
         gbs = p[2] / (p[0] * 1e-3) / 1e9
         fe = {'kernel': 'od_fe', 'clips': n_fe, 'clips_per_s': n_fe * p[1] / (p[0] * 1e-3),
               'roofline': {'bound': 'hbm', 'achieved': gbs, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-                           'frac': gbs / HBM_PEAK_GBS, 'traffic': None,
-                           'avg_launch_ms': p[0] / max(p[1], 1), 'bytes_per_clip': OD_FE_BYTES}}
+                           'frac': gbs / HBM_PEAK_GBS, 'avg_launch_ms': p[0] / max(p[1], 1),
+                           'bytes_per_clip': OD_FE_BYTES}}
+        fe['roofline']['traffic'], fe['roofline']['traffic_source'] = pmc_traffic('od_features', 'od_fe', n_fe)
 
-    cpu = None
     parity = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        n_s = 64
-        sample = pcm[:n_s].cpu().numpy() if pcm is not None else None
+    if rank == 0 and not args.no_parity:
         if wl == 'noise_gate':
-            cpu, e1 = cpu_baseline_nr(yf[:n_s].cpu().numpy(), noise_clip, nr_out[:n_s].cpu().numpy(),
-                                      args.cpu_seconds)
-            parity = {'nr_max_abs_err_vs_oracle': e1}
-        elif wl == 'si_pipeline':
-            feat = torch.empty((n_s, 256, 39), dtype=torch.float32, device='cuda')
-            ctx.si_features_dev(pcm.data_ptr(), n_s, clip_len, clip_len, feat.data_ptr())
-            torch.cuda.synchronize()
-            cpu, e1, e2 = cpu_baseline_si(sample, feat.cpu().numpy(), probs[:n_s].cpu().numpy(),
-                                          W_si, args.cpu_seconds)
-            parity = {'si_feature_max_abs_err': e1, 'prob_max_abs_err': e2}
+            from oracle import noisereduce as onr
+            idx = sample_indices(clips, clips, 6)[:8]
+            err = 0.0
+            for i in idx:
+                w = onr.reduce_noise(yf[i].cpu().numpy(), 16000, noise_clip)
+                err = max(err, float(np.abs(nr_out[i].cpu().numpy() - w).max()))
+            parity = {'sample_clips': len(idx), 'nr_max_abs_err_vs_oracle': err}
         else:
-            nrm = torch.empty((n_s, 128, 151), dtype=torch.float32, device='cuda')
-            ctx.od_features_dev(pcm.data_ptr(), n_s, clip_len, clip_len, norm=nrm.data_ptr())
-            torch.cuda.synchronize()
-            gp = probs[:n_s].cpu().numpy() if wl == 'od_pipeline' else np.zeros((n_s, 2))
-            cpu, e1, e2 = cpu_baseline_od(sample, nrm.cpu().numpy(), gp, W_od, args.cpu_seconds)
-            parity = {'od_norm_logmel_max_abs_err': e1}
-            if wl == 'od_pipeline':
-                parity['prob_max_abs_err'] = e2
+            parity = parity_sample(ctx, wl, pcm, probs, argmax, W, mb, clip_len)
 
+    devices = rank_devices(world, rank, local)
     if rank == 0:
         desc = {
             'od_pipeline': 'config 3: fused log-mel/ZCR front-end -> uint8 image -> OD-NET ResLSTM '
@@ -325,8 +374,8 @@ def main():
             'metric': METRIC, 'value': value, 'unit': 'clips/s', 'n_gpus': world,
             'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': dt / args.steps * 1e3,
             'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
-            # convolutions: error-compensated 3xFP16 on f16 MFMA with f32 accumulation; front-ends
-            # f32 (OD) / f64 (SI); LSTM, heads f32
+            # convolutions + LSTM: error-compensated 3xFP16 on f16 MFMA with f32 accumulation;
+            # front-ends f32 (OD) / f64 (SI); heads f32.  The exact-f32 run is `precision_f32`.
             'dtype': {'od_pipeline': 'f16x3+f32', 'si_pipeline': 'f64+f16x3',
                       'noise_gate': 'f64'}.get(wl, 'f32'),
             'data': (f'synthetic: {clips} x {clip_len / 16000:g} s 16 kHz clips per GPU generated in '
@@ -336,9 +385,11 @@ def main():
                       ' (int16); seeded synthetic weights in the reference variables.index layout '
                       '(trained blobs absent)')),
             'config': {'workload': f'{wl} ({desc})', 'clips_per_gpu': clips,
-                       'global_batch': world * clips, 'clip_samples': clip_len,
-                       'parallelism': f'dp{world}' + ('+rccl_allgather_logits' if world > 1 else '')},
-            'roofline': roof, 'stages': stages, 'fe': fe, 'cpu_baseline': cpu, 'parity': parity,
+                       'global_batch': world * clips, 'clip_samples': clip_len, 'microbatch': mb,
+                       'parallelism': f'dp{world}' + ('+rccl_allgather_logits' if world > 1 and pipeline else '')},
+            'world_size': world, 'gpus_requested': args.gpus, 'rank_devices': devices,
+            'roofline': roof, 'stages': stages, 'fe': fe, 'precision_f32': f32,
+            'range_guard_ok': range_ok, 'cpu_baseline': cpu, 'parity': parity,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

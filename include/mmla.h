@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define MMLA_ABI_VERSION 1
+#define MMLA_ABI_VERSION 2
 
 enum mmla_status {
   MMLA_OK = 0,
@@ -36,7 +36,8 @@ enum mmla_status {
   MMLA_E_HIP = -2,       /* HIP runtime error */
   MMLA_E_NOWEIGHTS = -3, /* forward called before mmla_load_weights for that model */
   MMLA_E_OOM = -4,       /* device allocation failed */
-  MMLA_E_SHAPE = -5      /* packed weight blob has the wrong number of floats */
+  MMLA_E_SHAPE = -5,     /* packed weight blob has the wrong number of floats */
+  MMLA_E_RANGE = -6      /* 3xFP16: an operand left the fp16 range in a device-pointer call */
 };
 
 enum mmla_model { MMLA_MODEL_OD = 0, MMLA_MODEL_SI = 1 };
@@ -61,21 +62,47 @@ int mmla_abi_version(void);
 int mmla_create(int device, mmla_ctx** out);
 int mmla_destroy(mmla_ctx* ctx);
 const char* mmla_last_error(const mmla_ctx* ctx);
-/* Use an external hipStream_t (e.g. torch.cuda.current_stream().cuda_stream); NULL = own stream. */
+/* Use an external hipStream_t (e.g. torch.cuda.current_stream().cuda_stream); NULL = the context's
+ * own stream, a blocking stream (it orders with the legacy NULL stream, i.e. with PyTorch's default
+ * stream; work on any other stream that produces a call's device inputs must be ordered by the
+ * caller, e.g. by passing that stream here).  The new stream first waits (hipStreamWaitEvent) for
+ * the work already enqueued on the old one, which still uses this context's workspaces. */
 int mmla_set_stream(mmla_ctx* ctx, void* hip_stream);
+/* Wait for the context stream; returns MMLA_E_RANGE (see mmla_range_check) if a device-pointer call
+ * since the last check overflowed the fp16 range. */
 int mmla_synchronize(mmla_ctx* ctx);
 /*
- * Arithmetic of the spatial convolutions (98 % of OD-NET FLOPs):
+ * Arithmetic of the spatial convolutions (98 % of OD-NET FLOPs) and the BiLSTM:
  *   MMLA_PREC_F16X3 (default) error-compensated 3xFP16 on f16 MFMA: operands split hi + 2^-11 lo,
  *                   hi*hi + hi*lo + lo*hi accumulated in f32 (~22-bit products, f32 accumulation);
- *                   requires |activations|, |weights| < 65504.
+ *                   needs |activations|, |weights| < 65504 (LSTM: |x| < 1023, |w| < 255.9).
+ *                   Range guard: weights outside it make that model run exact f32 (decided at
+ *                   mmla_load_weights); every kernel that splits an activation flags a value
+ *                   outside it.  Host-pointer calls then re-run the micro-batch in exact f32
+ *                   (counted by mmla_range_check); device-pointer calls report MMLA_E_RANGE from
+ *                   the next mmla_range_check / mmla_synchronize.
  *   MMLA_PREC_F32   exact f32 MFMA (v_mfma_f32_32x32x2_f32), 1/5.3 of the throughput.
- * LSTM, dense heads, 1x1 shortcuts and the front-ends are f32/f64 in both modes.
+ * 1x1 shortcuts, dense heads and the front-ends are f32/f64 in both modes.
  */
 enum mmla_precision { MMLA_PREC_F32 = 0, MMLA_PREC_F16X3 = 1 };
 int mmla_set_precision(mmla_ctx* ctx, int mode);
-/* Cap the clips processed per internal micro-batch (activation memory); 0 = default. */
+/* Waits for the context stream.  *f32_reruns (nullable) = host-pointer micro-batches re-run in
+ * exact f32 so far; returns MMLA_E_RANGE (and clears the flag) if a device-pointer call since the
+ * last check split an out-of-range operand -- its results are invalid. */
+int mmla_range_check(mmla_ctx* ctx, int64_t* f32_reruns);
+/*
+ * Clips per internal micro-batch (activation memory).  0 = sized at each call from the device's
+ * free memory, capped at 16384 (OD) / 65536 (SI) clips; an allocation failure halves it and
+ * retries.  Per-clip device footprint of a micro-batch: OD ~7.6 MB (three n*128*151*32 f32
+ * activation buffers + image + front-end scratch), so the 16384-clip default holds ~124 GB;
+ * SI ~0.14 MB (65536 clips ~9 GB).  Weights: OD ~12 MB, SI ~10 MB.  Workspaces are kept for
+ * reuse until mmla_release_workspace or mmla_destroy.
+ */
 int mmla_set_microbatch(mmla_ctx* ctx, int64_t od_clips, int64_t si_clips);
+/* The micro-batch sizes the next call would use. */
+int mmla_get_microbatch(mmla_ctx* ctx, int64_t* od_clips, int64_t* si_clips);
+/* Free every device workspace of the context (after its stream drains). */
+int mmla_release_workspace(mmla_ctx* ctx);
 
 /*
  * Load network weights from the packed float32 blob (host memory) in the canonical order of
@@ -137,10 +164,13 @@ int mmla_od_forward_u8(mmla_ctx* ctx, const uint8_t* img, int64_t n, float* prob
 int mmla_si_forward(mmla_ctx* ctx, const float* x, int64_t n, float* probs, uint32_t flags);
 
 /* Fused WAV->class pipelines (no PNG, no host round trip): probs [n,K] f32 (nullable),
- * argmax [n] i32 (nullable; -1 for SI 'silent' clips), silent [n] u8 (SI only, nullable). */
+ * argmax [n] i32 (nullable; -1 for 'silent' clips), silent [n] u8 (nullable).  'silent' = fewer
+ * than 4000 samples (lens[c], or clip_len without lens): OD record_on_pc.py:141-154 logs it and
+ * skips predict, SI speaker_identification.py:375-376 returns the 'silent' sentinel; their probs
+ * are still computed (on the zero-padded clip) but carry no meaning. */
 int mmla_od_pipeline(mmla_ctx* ctx, const int16_t* pcm, int64_t n_clips, int64_t clip_stride,
                      const int32_t* lens, int32_t clip_len, float* probs, int32_t* argmax,
-                     uint32_t flags);
+                     uint8_t* silent, uint32_t flags);
 int mmla_si_pipeline(mmla_ctx* ctx, const int16_t* pcm, int64_t n_clips, int64_t clip_stride,
                      const int32_t* lens, int32_t clip_len, float* probs, int32_t* argmax,
                      uint8_t* silent, uint32_t flags);

@@ -22,8 +22,9 @@ PREC_F32, PREC_F16X3 = 0, 1
 OD_MELS, OD_FRAMES, OD_CLIP = 128, 151, 24000
 SI_FRAMES, SI_DIMS, SI_SILENT_LEN = 256, 39, 4000
 
+MMLA_E_RANGE = -6
 _ERRORS = {-1: 'MMLA_E_INVALID', -2: 'MMLA_E_HIP', -3: 'MMLA_E_NOWEIGHTS', -4: 'MMLA_E_OOM',
-           -5: 'MMLA_E_SHAPE'}
+           -5: 'MMLA_E_SHAPE', -6: 'MMLA_E_RANGE'}
 
 _P = ctypes.c_void_p
 _I64 = ctypes.c_int64
@@ -40,6 +41,9 @@ SIGNATURES = {
     'mmla_set_stream': [_P, _P],
     'mmla_synchronize': [_P],
     'mmla_set_microbatch': [_P, _I64, _I64],
+    'mmla_get_microbatch': [_P, ctypes.POINTER(_I64), ctypes.POINTER(_I64)],
+    'mmla_release_workspace': [_P],
+    'mmla_range_check': [_P, ctypes.POINTER(_I64)],
     'mmla_set_precision': [_P, ctypes.c_int],
     'mmla_load_weights': [_P, ctypes.c_int, _P, _I64, _I32, _I32],
     'mmla_od_features': [_P, _P, _I64, _I64, _P, _I32, _P, _P, _P, _P, _U32],
@@ -48,7 +52,7 @@ SIGNATURES = {
     'mmla_od_forward': [_P, _P, _I64, _P, _U32],
     'mmla_od_forward_u8': [_P, _P, _I64, _P, _U32],
     'mmla_si_forward': [_P, _P, _I64, _P, _U32],
-    'mmla_od_pipeline': [_P, _P, _I64, _I64, _P, _I32, _P, _P, _U32],
+    'mmla_od_pipeline': [_P, _P, _I64, _I64, _P, _I32, _P, _P, _P, _U32],
     'mmla_si_pipeline': [_P, _P, _I64, _I64, _P, _I32, _P, _P, _P, _U32],
     'mmla_profile_enable': [_P, ctypes.c_int],
     'mmla_profile_read': [_P, _P, _P, _P, ctypes.c_int],
@@ -99,7 +103,9 @@ def _ptr(a):
 
 
 class MmlaError(RuntimeError):
-    pass
+    def __init__(self, msg, code=None):
+        super().__init__(msg)
+        self.code = code
 
 
 class Context:
@@ -135,7 +141,7 @@ class Context:
     def _check(self, rc, what):
         if rc != MMLA_OK:
             msg = self.lib.mmla_last_error(self.h)
-            raise MmlaError(f'{what}: {_ERRORS.get(rc, rc)}: {msg.decode() if msg else ""}')
+            raise MmlaError(f'{what}: {_ERRORS.get(rc, rc)}: {msg.decode() if msg else ""}', rc)
 
     # -- configuration ------------------------------------------------------------------------
     def set_stream(self, stream_handle):
@@ -150,6 +156,23 @@ class Context:
 
     def set_microbatch(self, od=0, si=0):
         self._check(self.lib.mmla_set_microbatch(self.h, int(od), int(si)), 'mmla_set_microbatch')
+
+    def get_microbatch(self):
+        """-> (od_clips, si_clips) per internal micro-batch for the next call."""
+        od, si = _I64(), _I64()
+        self._check(self.lib.mmla_get_microbatch(self.h, ctypes.byref(od), ctypes.byref(si)),
+                    'mmla_get_microbatch')
+        return od.value, si.value
+
+    def release_workspace(self):
+        self._check(self.lib.mmla_release_workspace(self.h), 'mmla_release_workspace')
+
+    def range_check(self):
+        """Wait for the stream; -> number of host-call micro-batches re-run in exact f32 so far.
+        Raises MmlaError (code MMLA_E_RANGE) if a device-pointer call overflowed the fp16 range."""
+        n = _I64()
+        self._check(self.lib.mmla_range_check(self.h, ctypes.byref(n)), 'mmla_range_check')
+        return n.value
 
     def profile_enable(self, on=True):
         self._check(self.lib.mmla_profile_enable(self.h, int(bool(on))), 'mmla_profile_enable')
@@ -284,13 +307,16 @@ class Context:
         return probs
 
     def od_pipeline(self, pcm, lens=None):
+        """-> (probs [n,2], argmax [n] (-1 = 'silent'), silent [n] bool)."""
         a, ln, L = self._pcm(pcm, lens)
         n = a.shape[0]
         probs = np.empty((n, 2), np.float32)
         am = np.empty(n, np.int32)
+        silent = np.empty(n, np.uint8)
         self._check(self.lib.mmla_od_pipeline(self.h, _ptr(a), n, a.shape[1], _ptr(ln), L,
-                                              _ptr(probs), _ptr(am), 0), 'mmla_od_pipeline')
-        return probs, am
+                                              _ptr(probs), _ptr(am), _ptr(silent), 0),
+                    'mmla_od_pipeline')
+        return probs, am, silent.astype(bool)
 
     def od_pipeline_strided(self, signal, n, stride, clip_len):
         """OD pipeline over n windows of one long int16 signal: window c = signal[c*stride :
@@ -301,7 +327,7 @@ class Context:
         probs = np.empty((n, 2), np.float32)
         am = np.empty(n, np.int32)
         self._check(self.lib.mmla_od_pipeline(self.h, _ptr(sig), n, stride, None, clip_len,
-                                              _ptr(probs), _ptr(am), 0), 'mmla_od_pipeline')
+                                              _ptr(probs), _ptr(am), None, 0), 'mmla_od_pipeline')
         return probs, am
 
     def si_pipeline(self, pcm, lens=None):
@@ -326,9 +352,10 @@ class Context:
                                               silent or None, MMLA_DEVICE_PTR),
                     'mmla_si_features(dev)')
 
-    def od_pipeline_dev(self, pcm, n, stride, clip_len, probs=0, argmax=0, lens=0):
+    def od_pipeline_dev(self, pcm, n, stride, clip_len, probs=0, argmax=0, lens=0, silent=0):
         self._check(self.lib.mmla_od_pipeline(self.h, pcm, n, stride, lens or None, clip_len,
-                                              probs or None, argmax or None, MMLA_DEVICE_PTR),
+                                              probs or None, argmax or None, silent or None,
+                                              MMLA_DEVICE_PTR),
                     'mmla_od_pipeline(dev)')
 
     def si_pipeline_dev(self, pcm, n, stride, clip_len, probs=0, argmax=0, silent=0, lens=0):

@@ -80,8 +80,18 @@ struct ProfRec {
 
 }  // namespace
 
-constexpr int64_t kOdMicrobatch = 16384;   // OD clips per internal micro-batch (122 GB of activations; 4096: -2.4 % clips/s)
-constexpr int64_t kSiMicrobatch = 65536;   // SI clips per micro-batch (16384: -4 % clips/s, layer tails)
+// Micro-batch caps (clips per internal pass).  The default (mmla_set_microbatch 0) is sized from
+// the device's free memory at call time, capped here: 16384 OD clips = 124 GB of activations
+// (4096: -2.4 % clips/s), 65536 SI clips = 9 GB (16384: -4 %).  A micro-batch whose workspace
+// allocation fails is halved and retried (down to kMinMicrobatch) instead of failing the call.
+constexpr int64_t kOdMicrobatch = 16384;
+constexpr int64_t kSiMicrobatch = 65536;
+constexpr int64_t kMinMicrobatch = 64;
+// device bytes per clip of one micro-batch (workspace slots of run_od_net / run_si_net + FE I/O)
+constexpr double kOdBytesPerClip = 3.0 * 128 * 151 * 32 * 4 + 128 * 151 * 3 + 128 * 151 * 4 +
+                                   19 * 128 * 4 + 512 * 4 + 64;
+constexpr double kSiBytesPerClip = 4.0 * 256 * 32 * 4 + 256 * 39 * 4 + 8 * 128 * 4 + 512 * 4 +
+                                   1024 * 4 + 64;
 
 struct mmla_ctx {
   bool prof_on = false;
@@ -103,8 +113,18 @@ struct mmla_ctx {
   std::vector<void*> ws;
   std::vector<size_t> ws_size;
   std::vector<size_t> ws_guard;   // MMLA_WS_GUARD: guard bytes before and after each slot (0 = none)
-  int64_t od_mb = kOdMicrobatch, si_mb = kSiMicrobatch;
+  int64_t od_mb = 0, si_mb = 0;            // user caps (0 = sized from free memory)
+  int64_t od_mb_cap = kOdMicrobatch, si_mb_cap = kSiMicrobatch;   // lowered after an OOM retry
   int precision = MMLA_PREC_F16X3;
+  // 3xFP16 range guard: kernels set range_dev[0] (device-pointer calls; sticky until
+  // mmla_range_check) or range_dev[1] (host-pointer micro-batches: re-run in exact f32) when an
+  // operand they split into fp16 is >= 65504 in magnitude or not finite
+  int* range_dev = nullptr;
+  int* range_host = nullptr;                // pinned copy of range_dev[1]
+  int* range_ptr = nullptr;                 // what the current launches write (null: unguarded)
+  int64_t range_reruns = 0;
+  bool od_f32_only = false, si_f32_only = false;   // weights outside the fp16 range
+  bool loading_f16_bad = false;                     // mmla_load_weights scratch
   NrTables* nr_tables = nullptr;   // noise gate (nr.hip): tables + the noise profile's threshold
   float* nr_thresh = nullptr;
   bool nr_ready = false;
@@ -199,27 +219,44 @@ int ws_get(mmla_ctx* c, int slot, size_t bytes, void** out) {
     c->ws_size.resize(slot + 1, 0);
     c->ws_guard.resize(slot + 1, 0);
   }
-  if (c->ws_size[slot] < bytes) {
+  const char* ge = std::getenv("MMLA_WS_GUARD");
+  const size_t guard = ge && ge[0] == '1' ? kGuardBytes : 0;
+  // guarded slots are re-framed whenever the size changes, so the trailing band always sits right
+  // behind the live tensor (not behind the largest one ever requested)
+  if (c->ws_size[slot] < bytes || (guard && c->ws_size[slot] != bytes)) {
     if (c->ws[slot]) {
       HIPCHK(c, hipStreamSynchronize(c->stream));
       HIPCHK(c, hipFree(static_cast<char*>(c->ws[slot]) - c->ws_guard[slot]));
       c->ws[slot] = nullptr;
       c->ws_size[slot] = 0;
     }
-    const char* ge = std::getenv("MMLA_WS_GUARD");
-    const size_t guard = ge && ge[0] == '1' ? kGuardBytes : 0;
     void* p = nullptr;
-    if (hipMalloc(&p, bytes + 2 * guard) != hipSuccess)
+    if (hipMalloc(&p, bytes + 2 * guard) != hipSuccess) {
+      (void)hipGetLastError();   // clear the sticky allocation error
       return fail(c, MMLA_E_OOM, "hipMalloc(%zu) failed for workspace slot %d", bytes, slot);
-    if (guard) {
-      HIPCHK(c, hipMemset(p, kGuardByte, guard));
-      HIPCHK(c, hipMemset(static_cast<char*>(p) + guard + bytes, kGuardByte, guard));
+    }
+    if (guard) {   // on the context stream: ordered before the kernels that follow
+      HIPCHK(c, hipMemsetAsync(p, kGuardByte, guard, c->stream));
+      HIPCHK(c, hipMemsetAsync(static_cast<char*>(p) + guard + bytes, kGuardByte, guard, c->stream));
     }
     c->ws[slot] = static_cast<char*>(p) + guard;
     c->ws_size[slot] = bytes;
     c->ws_guard[slot] = guard;
   }
   *out = c->ws[slot];
+  return MMLA_OK;
+}
+
+// free every workspace slot (after the stream drains)
+int ws_release(mmla_ctx* c) {
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  for (size_t i = 0; i < c->ws.size(); ++i)
+    if (c->ws[i]) {
+      HIPCHK(c, hipFree(static_cast<char*>(c->ws[i]) - c->ws_guard[i]));
+      c->ws[i] = nullptr;
+      c->ws_size[i] = 0;
+      c->ws_guard[i] = 0;
+    }
   return MMLA_OK;
 }
 
@@ -278,6 +315,8 @@ int take_conv(mmla_ctx* c, Cursor& cur, std::vector<void*>& al, int kh, int kw, 
   const float* k = cur.take((int64_t)kh * kw * cin * cout);
   const float* b = cur.take(cout);
   if (!cur.ok) return fail(c, MMLA_E_SHAPE, "weight blob too short");
+  for (int64_t i = 0; i < (int64_t)kh * kw * cin * cout; ++i)
+    if (!(std::fabs(k[i]) < 65504.0f)) c->loading_f16_bad = true;   // 3xFP16 needs fp16-range w
   w->kh = kh;
   w->kw = kw;
   w->cin = cin;
@@ -346,6 +385,7 @@ int take_lstm(mmla_ctx* c, Cursor& cur, std::vector<void*>& al, int d, LstmW* l)
     memcpy(wc.data() + 256 * 1024, k, sizeof(float) * d * 1024);
     CHK(upload(c, al, wc.data(), wc.size() * sizeof(float), &l->wcat[dir]));
     CHK(upload(c, al, b, 1024 * sizeof(float), &l->bias[dir]));
+    if (!bilstm_h3_weights_in_range(wc.data(), d)) c->loading_f16_bad = true;
     std::vector<uint16_t> hi(wc.size()), lo(wc.size());
     bilstm_h3_split_weights(wc.data(), d, hi.data(), lo.data());
     float* p = nullptr;
@@ -439,6 +479,85 @@ int finish(mmla_ctx* c, bool dev) {
   return MMLA_OK;
 }
 
+// ---- micro-batching and the 3xFP16 range guard -------------------------------------------------
+
+// clips per micro-batch: the user's cap, else what the device's free memory holds (the slots this
+// context already owns count as free), capped at the default / the cap left by an OOM retry
+int64_t microbatch(mmla_ctx* c, bool od) {
+  const int64_t user = od ? c->od_mb : c->si_mb;
+  if (user > 0) return user;
+  const int64_t cap = od ? c->od_mb_cap : c->si_mb_cap;
+  size_t fr = 0, tot = 0;
+  if (hipMemGetInfo(&fr, &tot) != hipSuccess) {
+    (void)hipGetLastError();
+    return cap;
+  }
+  double held = 0;
+  for (size_t b : c->ws_size) held += (double)b;
+  int64_t fit = (int64_t)(((double)fr + held) * 0.9 / (od ? kOdBytesPerClip : kSiBytesPerClip));
+  fit = fit / kMinMicrobatch * kMinMicrobatch;
+  return std::max(kMinMicrobatch, std::min(cap, fit));
+}
+
+// body(c0, cnt) over clips [0, n) in micro-batches.  A workspace allocation failure (MMLA_E_OOM)
+// frees the context's workspaces, halves the micro-batch (unless the caller fixed it with
+// mmla_set_microbatch) and retries the same clips.
+template <class F>
+int for_microbatches(mmla_ctx* c, bool od, int64_t n, F&& body) {
+  int64_t c0 = 0;
+  int64_t mb = microbatch(c, od);   // fixed for the call (unless an allocation fails)
+  while (c0 < n) {
+    const int64_t cnt = std::min(mb, n - c0);
+    const int rc = body(c0, cnt);
+    if (rc == MMLA_E_OOM && (od ? c->od_mb : c->si_mb) == 0 && cnt > kMinMicrobatch) {
+      CHK(ws_release(c));
+      mb = std::max(kMinMicrobatch, cnt / 2);
+      (od ? c->od_mb_cap : c->si_mb_cap) = mb;
+      continue;
+    }
+    CHK(rc);
+    c0 += cnt;
+  }
+  return MMLA_OK;
+}
+
+// one micro-batch of a network call under the 3xFP16 range guard.  Device-pointer calls let the
+// kernels flag into range_dev[0] (sticky, reported by mmla_range_check / mmla_synchronize);
+// host-pointer calls check range_dev[1] after the micro-batch and re-run it in exact f32 when an
+// operand left the fp16 range.  f32_only: the model's weights are outside the fp16 range.
+template <class F>
+int guarded(mmla_ctx* c, bool dev, bool f32_only, F&& body) {
+  struct Restore {   // precision and flag target of the context, restored on every return
+    mmla_ctx* c;
+    int prec;
+    ~Restore() {
+      c->precision = prec;
+      c->range_ptr = nullptr;
+    }
+  } restore{c, c->precision};
+  if (f32_only) c->precision = MMLA_PREC_F32;
+  if (c->precision != MMLA_PREC_F16X3) {
+    c->range_ptr = nullptr;
+    return body();
+  }
+  if (dev) {
+    c->range_ptr = c->range_dev;
+    return body();
+  }
+  c->range_ptr = c->range_dev + 1;
+  HIPCHK(c, hipMemsetAsync(c->range_ptr, 0, sizeof(int), c->stream));
+  CHK(body());
+  HIPCHK(c, hipMemcpyAsync(c->range_host, c->range_ptr, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (*c->range_host) {
+    c->precision = MMLA_PREC_F32;
+    c->range_ptr = nullptr;
+    c->range_reruns += 1;
+    CHK(body());
+  }
+  return MMLA_OK;
+}
+
 // ---- network runners (device pointers, one micro-batch) -----------------------------------------
 
 ConvArgs conv_args(const ConvW& w, const float* x, float* y, int n, int h, int wd, int stride,
@@ -512,6 +631,7 @@ int conv_spatial(mmla_ctx* c, const ConvW& w, const float* x, float* y, int n, i
     a.pro = pro;
     a.epi = epi;
     a.pool_out = pool_out ? 1 : 0;
+    a.range_flag = c->range_ptr;
     LAUNCH(c, MMLA_STAGE_CONV, 2.0 * n * h * wd * w.kh * w.kw * w.cin * w.cout,
            conv_h3_launch(a, c->stream));
     return MMLA_OK;
@@ -527,16 +647,25 @@ double lstm_flops(int64_t n, int T, int D) { return 2.0 * n * T * 2 * (256.0 + D
 hipError_t lstm_run(mmla_ctx* c, const LstmW& L, const float* seq, int64_t n, int T, float* out) {
   if (c->precision == MMLA_PREC_F16X3 && L.wth[0])
     return bilstm_h3_launch(seq, (int)n, T, 128, L.wth[0], L.wtl[0], L.wth[1], L.wtl[1], L.bias[0],
-                            L.bias[1], out, c->stream);
+                            L.bias[1], out, c->range_ptr, c->stream);
   return bilstm_launch(seq, (int)n, T, 128, L.wcat[0], L.wcat[1], L.bias[0], L.bias[1], out,
                        c->stream);
 }
+
+// the OD 'silent' gate (record_on_pc.py:141-154) of one micro-batch: device lens (nullable) or
+// clip_len; silent output (nullable)
+struct OdGate {
+  const int32_t* lens = nullptr;
+  int clip_len = -1;   // < 0: no gate (network-only calls)
+  uint8_t* silent = nullptr;
+};
 
 // OD-NET on a device batch; input = uint8 image (img_u8) or float NHWC (img_f32).
 // `stop` >= 0 (debug trace): return after stage `stop` (0 stem, 1..9 res blocks, 10 mean, 11
 // BiLSTM) with *tap / *tap_n set to that stage's output tensor.
 int run_od_net(mmla_ctx* c, const uint8_t* img_u8, const float* img_f32, int64_t n, float* probs,
-               int32_t* argmax, int stop = -1, const float** tap = nullptr, int64_t* tap_n = nullptr) {
+               int32_t* argmax, OdGate gate = OdGate(), int stop = -1, const float** tap = nullptr,
+               int64_t* tap_n = nullptr) {
   const OdNet& W = c->od;
   const size_t big = (size_t)n * OD_PIX * 32 * sizeof(float);
   void *px, *pt1, *pt2, *pseq, *ph;
@@ -598,6 +727,7 @@ int run_od_net(mmla_ctx* c, const uint8_t* img_u8, const float* img_f32, int64_t
       r.n = (int)n;
       r.h = h;
       r.w = w;
+      r.range_flag = c->range_ptr;
       LAUNCH(c, MMLA_STAGE_CONV,
              (b == 0 && fuse_stem ? 2.0 * n * h * w * 3 * 16 : 0.0) +
              2.0 * n * h * w * (9.0 * B.c3.cin * B.c3.cout + 4.0 * B.c4.cin * B.c4.cout) +
@@ -660,7 +790,7 @@ int run_od_net(mmla_ctx* c, const uint8_t* img_u8, const float* img_f32, int64_t
   }
   LAUNCH(c, MMLA_STAGE_HEAD, 2.0 * n * 512 * 2,
          od_head_launch(static_cast<float*>(ph), (int)n, W.head_w, W.head_b, probs, argmax,
-                        c->stream));
+                        gate.lens, gate.clip_len, gate.silent, c->stream));
   return MMLA_OK;
 }
 
@@ -760,11 +890,21 @@ int mmla_create(int device, mmla_ctx** out) {
   if (hipSetDevice(device) != hipSuccess) return MMLA_E_HIP;
   mmla_ctx* c = new mmla_ctx();
   c->device = device;
-  if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) {
+  // a BLOCKING stream: it orders with the legacy default (NULL) stream, on which PyTorch's default
+  // stream enqueues -- so a device-pointer call sees tensors a torch kernel or copy just produced
+  // without an explicit synchronisation (a non-blocking stream raced them: a 65 536-clip call read
+  // the last clips before torch had written them)
+  if (hipStreamCreateWithFlags(&c->own_stream, hipStreamDefault) != hipSuccess) {
     delete c;
     return MMLA_E_HIP;
   }
   c->stream = c->own_stream;
+  if (hipMalloc(&c->range_dev, 2 * sizeof(int)) != hipSuccess ||
+      hipMemset(c->range_dev, 0, 2 * sizeof(int)) != hipSuccess ||
+      hipHostMalloc(&c->range_host, sizeof(int), hipHostMallocDefault) != hipSuccess) {
+    mmla_destroy(c);
+    return MMLA_E_HIP;
+  }
   OdFeTables ot;
   od_fe_build_tables(&ot);
   if (!od_fe_tables_ok(ot)) {   // mel tap counts exceed the front-end kernel's unrolled taps
@@ -800,6 +940,8 @@ int mmla_destroy(mmla_ctx* c) {
   if (c->si_tables) (void)hipFree(c->si_tables);
   if (c->nr_tables) (void)hipFree(c->nr_tables);
   if (c->nr_thresh) (void)hipFree(c->nr_thresh);
+  if (c->range_dev) (void)hipFree(c->range_dev);
+  if (c->range_host) (void)hipHostFree(c->range_host);
   (void)prof_collect(c);
   for (hipEvent_t e : c->prof_pool) (void)hipEventDestroy(e);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
@@ -932,14 +1074,55 @@ const char* mmla_last_error(const mmla_ctx* c) { return c ? c->err.c_str() : "nu
 
 int mmla_set_stream(mmla_ctx* c, void* s) {
   if (!c) return MMLA_E_INVALID;
-  c->stream = s ? static_cast<hipStream_t>(s) : c->own_stream;
+  hipStream_t ns = s ? static_cast<hipStream_t>(s) : c->own_stream;
+  if (ns != c->stream) {
+    // work already enqueued on the old stream still reads and writes this context's workspaces:
+    // the new stream waits for it before the next call reuses them
+    HIPCHK(c, hipSetDevice(c->device));
+    hipEvent_t e = nullptr;
+    HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    const hipError_t r1 = hipEventRecord(e, c->stream);
+    const hipError_t r2 = r1 == hipSuccess ? hipStreamWaitEvent(ns, e, 0) : r1;
+    (void)hipEventDestroy(e);
+    HIPCHK(c, r2);
+  }
+  c->stream = ns;
+  return MMLA_OK;
+}
+
+int mmla_range_check(mmla_ctx* c, int64_t* f32_reruns) {
+  if (!c) return MMLA_E_INVALID;
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (f32_reruns) *f32_reruns = c->range_reruns;
+  int flag = 0;
+  HIPCHK(c, hipMemcpy(&flag, c->range_dev, sizeof(int), hipMemcpyDeviceToHost));
+  if (flag) {
+    HIPCHK(c, hipMemset(c->range_dev, 0, sizeof(int)));
+    return fail(c, MMLA_E_RANGE,
+                "a device-pointer call since the last check split an operand outside the fp16 "
+                "range (|x| >= 65504): its results are not valid; re-run it with MMLA_PREC_F32");
+  }
   return MMLA_OK;
 }
 
 int mmla_synchronize(mmla_ctx* c) {
   if (!c) return MMLA_E_INVALID;
-  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return mmla_range_check(c, nullptr);
+}
+
+int mmla_get_microbatch(mmla_ctx* c, int64_t* od_clips, int64_t* si_clips) {
+  if (!c) return MMLA_E_INVALID;
+  HIPCHK(c, hipSetDevice(c->device));
+  if (od_clips) *od_clips = microbatch(c, true);
+  if (si_clips) *si_clips = microbatch(c, false);
   return MMLA_OK;
+}
+
+int mmla_release_workspace(mmla_ctx* c) {
+  if (!c) return MMLA_E_INVALID;
+  HIPCHK(c, hipSetDevice(c->device));
+  return ws_release(c);
 }
 
 int mmla_set_precision(mmla_ctx* c, int mode) {
@@ -950,8 +1133,10 @@ int mmla_set_precision(mmla_ctx* c, int mode) {
 
 int mmla_set_microbatch(mmla_ctx* c, int64_t od, int64_t si) {
   if (!c || od < 0 || si < 0) return MMLA_E_INVALID;
-  c->od_mb = od ? od : kOdMicrobatch;   // 0 = the default (mmla.h)
-  c->si_mb = si ? si : kSiMicrobatch;
+  c->od_mb = od;   // 0 = sized from free memory (mmla.h)
+  c->si_mb = si;
+  c->od_mb_cap = kOdMicrobatch;
+  c->si_mb_cap = kSiMicrobatch;
   return MMLA_OK;
 }
 
@@ -962,6 +1147,7 @@ int mmla_load_weights(mmla_ctx* c, int kind, const float* packed, int64_t n_floa
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   Cursor cur{packed, n_floats};
+  c->loading_f16_bad = false;
   if (kind == MMLA_MODEL_OD) {
     if (n_classes != 2) return fail(c, MMLA_E_INVALID, "OD model has 2 classes, got %d", n_classes);
     free_allocs(c->od_allocs);
@@ -987,6 +1173,7 @@ int mmla_load_weights(mmla_ctx* c, int kind, const float* packed, int64_t n_floa
     CHK(upload(c, al, hb, 2 * sizeof(float), &W.head_b));
     if (cur.left != 0)
       return fail(c, MMLA_E_SHAPE, "OD weight blob has %lld extra floats", (long long)cur.left);
+    c->od_f32_only = c->loading_f16_bad;   // some weight outside the fp16 range: exact f32 only
     c->od_loaded = true;
     return MMLA_OK;
   }
@@ -1016,6 +1203,7 @@ int mmla_load_weights(mmla_ctx* c, int kind, const float* packed, int64_t n_floa
       return fail(c, MMLA_E_SHAPE, "SI weight blob has %lld extra floats", (long long)cur.left);
     W.k = n_classes;
     W.head = head;
+    c->si_f32_only = c->loading_f16_bad;
     c->si_loaded = true;
     return MMLA_OK;
   }
@@ -1029,9 +1217,7 @@ int mmla_od_features(mmla_ctx* c, const int16_t* pcm, int64_t n, int64_t stride,
   if (bad_pcm_args(pcm, n, stride, lens, clip_len)) return fail(c, MMLA_E_INVALID, "bad pcm args");
   HIPCHK(c, hipSetDevice(c->device));
   const bool dev = flags & MMLA_DEVICE_PTR;
-  const int64_t mb = dev ? std::max<int64_t>(n, 1) : c->od_mb;
-  for (int64_t c0 = 0; c0 < n; c0 += mb) {
-    const int64_t cnt = std::min(mb, n - c0);
+  auto body = [&](int64_t c0, int64_t cnt) -> int {
     Pcm p;
     CHK(stage_pcm(c, pcm, c0, cnt, stride, lens, clip_len, MMLA_OD_CLIP, dev, &p));
     OdFeArgs a{};
@@ -1053,6 +1239,12 @@ int mmla_od_features(mmla_ctx* c, const int16_t* pcm, int64_t n, int64_t stride,
     CHK(copy_back(c, zcr, c0 * OD_W, a.zcr, cnt * OD_W, dev));
     CHK(copy_back(c, img, c0 * OD_IMG, a.img, cnt * OD_IMG, dev));
     if (!dev) HIPCHK(c, hipStreamSynchronize(c->stream));
+    return MMLA_OK;
+  };
+  if (dev) {   // one launch over the caller's device buffers
+    if (n > 0) CHK(body(0, n));
+  } else {
+    CHK(for_microbatches(c, true, n, body));
   }
   return finish(c, dev);
 }
@@ -1065,9 +1257,7 @@ int mmla_si_features(mmla_ctx* c, const int16_t* pcm, int64_t n, int64_t stride,
     return fail(c, MMLA_E_INVALID, "bad pcm/feat args");
   HIPCHK(c, hipSetDevice(c->device));
   const bool dev = flags & MMLA_DEVICE_PTR;
-  const int64_t mb = dev ? std::max<int64_t>(n, 1) : c->si_mb;
-  for (int64_t c0 = 0; c0 < n; c0 += mb) {
-    const int64_t cnt = std::min(mb, n - c0);
+  auto body = [&](int64_t c0, int64_t cnt) -> int {
     Pcm p;
     CHK(stage_pcm(c, pcm, c0, cnt, stride, lens, clip_len, SI_NEED_SAMPLES, dev, &p));
     SiFeArgs a{};
@@ -1082,6 +1272,12 @@ int mmla_si_features(mmla_ctx* c, const int16_t* pcm, int64_t n, int64_t stride,
     CHK(copy_back(c, feat, c0 * SI_T * SI_D, a.feat, cnt * SI_T * SI_D, dev));
     CHK(copy_back(c, silent, c0, a.silent, cnt, dev));
     if (!dev) HIPCHK(c, hipStreamSynchronize(c->stream));
+    return MMLA_OK;
+  };
+  if (dev) {
+    if (n > 0) CHK(body(0, n));
+  } else {
+    CHK(for_microbatches(c, false, n, body));
   }
   return finish(c, dev);
 }
@@ -1113,52 +1309,48 @@ int mmla_si_features_seq(mmla_ctx* c, const int16_t* pcm, int64_t n_samples, int
   return finish(c, dev);
 }
 
-int mmla_od_forward(mmla_ctx* c, const float* x, int64_t n, float* probs, uint32_t flags) {
-  if (!c) return MMLA_E_INVALID;
-  if (n < 0 || (n > 0 && (!x || !probs))) return fail(c, MMLA_E_INVALID, "bad od_forward args");
+// OD-NET over float NHWC (x_f32) or uint8 (x_u8) images
+static int od_forward_common(mmla_ctx* c, const float* x_f32, const uint8_t* x_u8, int64_t n, float* probs,
+                      uint32_t flags) {
+  if (n < 0 || (n > 0 && ((!x_f32 && !x_u8) || !probs)))
+    return fail(c, MMLA_E_INVALID, "bad od_forward args");
   if (!c->od_loaded) return fail(c, MMLA_E_NOWEIGHTS, "OD weights not loaded");
   HIPCHK(c, hipSetDevice(c->device));
   const bool dev = flags & MMLA_DEVICE_PTR;
-  for (int64_t c0 = 0; c0 < n; c0 += c->od_mb) {
-    const int64_t cnt = std::min(c->od_mb, n - c0);
-    const float* dx = x + c0 * OD_IMG;
-    if (!dev) {
-      void* p = nullptr;
-      CHK(ws_get(c, S_IN, cnt * OD_IMG * sizeof(float), &p));
-      HIPCHK(c, hipMemcpyAsync(p, dx, cnt * OD_IMG * sizeof(float), hipMemcpyHostToDevice, c->stream));
-      dx = static_cast<float*>(p);
-    }
-    float* dp;
-    CHK(out_ptr(c, probs, c0 * 2, cnt * 2, dev, S_OUT0, &dp));
-    CHK(run_od_net(c, nullptr, dx, cnt, dp, nullptr));
-    CHK(copy_back(c, probs, c0 * 2, dp, cnt * 2, dev));
-    if (!dev) HIPCHK(c, hipStreamSynchronize(c->stream));
-  }
+  CHK(for_microbatches(c, true, n, [&](int64_t c0, int64_t cnt) -> int {
+    return guarded(c, dev, c->od_f32_only, [&]() -> int {
+      const float* df = x_f32 ? x_f32 + c0 * OD_IMG : nullptr;
+      const uint8_t* du = x_u8 ? x_u8 + c0 * OD_IMG : nullptr;
+      if (!dev) {
+        void* p = nullptr;
+        const size_t bytes = cnt * OD_IMG * (x_f32 ? sizeof(float) : 1);
+        CHK(ws_get(c, x_f32 ? S_IN : S_IMG, bytes, &p));
+        HIPCHK(c, hipMemcpyAsync(p, x_f32 ? (const void*)df : (const void*)du, bytes,
+                                 hipMemcpyHostToDevice, c->stream));
+        if (x_f32) df = static_cast<float*>(p);
+        else du = static_cast<uint8_t*>(p);
+      }
+      float* dp;
+      CHK(out_ptr(c, probs, c0 * 2, cnt * 2, dev, S_OUT0, &dp));
+      CHK(run_od_net(c, du, df, cnt, dp, nullptr));
+      CHK(copy_back(c, probs, c0 * 2, dp, cnt * 2, dev));
+      if (!dev) HIPCHK(c, hipStreamSynchronize(c->stream));
+      return MMLA_OK;
+    });
+  }));
   return finish(c, dev);
+}
+
+int mmla_od_forward(mmla_ctx* c, const float* x, int64_t n, float* probs, uint32_t flags) {
+  if (!c) return MMLA_E_INVALID;
+  if (n > 0 && !x) return fail(c, MMLA_E_INVALID, "bad od_forward args");
+  return od_forward_common(c, x, nullptr, n, probs, flags);
 }
 
 int mmla_od_forward_u8(mmla_ctx* c, const uint8_t* img, int64_t n, float* probs, uint32_t flags) {
   if (!c) return MMLA_E_INVALID;
-  if (n < 0 || (n > 0 && (!img || !probs))) return fail(c, MMLA_E_INVALID, "bad od_forward args");
-  if (!c->od_loaded) return fail(c, MMLA_E_NOWEIGHTS, "OD weights not loaded");
-  HIPCHK(c, hipSetDevice(c->device));
-  const bool dev = flags & MMLA_DEVICE_PTR;
-  for (int64_t c0 = 0; c0 < n; c0 += c->od_mb) {
-    const int64_t cnt = std::min(c->od_mb, n - c0);
-    const uint8_t* di = img + c0 * OD_IMG;
-    if (!dev) {
-      void* p = nullptr;
-      CHK(ws_get(c, S_IMG, cnt * OD_IMG, &p));
-      HIPCHK(c, hipMemcpyAsync(p, di, cnt * OD_IMG, hipMemcpyHostToDevice, c->stream));
-      di = static_cast<uint8_t*>(p);
-    }
-    float* dp;
-    CHK(out_ptr(c, probs, c0 * 2, cnt * 2, dev, S_OUT0, &dp));
-    CHK(run_od_net(c, di, nullptr, cnt, dp, nullptr));
-    CHK(copy_back(c, probs, c0 * 2, dp, cnt * 2, dev));
-    if (!dev) HIPCHK(c, hipStreamSynchronize(c->stream));
-  }
-  return finish(c, dev);
+  if (n > 0 && !img) return fail(c, MMLA_E_INVALID, "bad od_forward args");
+  return od_forward_common(c, nullptr, img, n, probs, flags);
 }
 
 int mmla_si_forward(mmla_ctx* c, const float* x, int64_t n, float* probs, uint32_t flags) {
@@ -1168,59 +1360,70 @@ int mmla_si_forward(mmla_ctx* c, const float* x, int64_t n, float* probs, uint32
   HIPCHK(c, hipSetDevice(c->device));
   const bool dev = flags & MMLA_DEVICE_PTR;
   const int k = c->si.k;
-  for (int64_t c0 = 0; c0 < n; c0 += c->si_mb) {
-    const int64_t cnt = std::min(c->si_mb, n - c0);
-    const float* dx = x + c0 * SI_T * SI_D;
-    if (!dev) {
-      void* p = nullptr;
-      CHK(ws_get(c, S_IN, cnt * SI_T * SI_D * sizeof(float), &p));
-      HIPCHK(c, hipMemcpyAsync(p, dx, cnt * SI_T * SI_D * sizeof(float), hipMemcpyHostToDevice,
-                               c->stream));
-      dx = static_cast<float*>(p);
-    }
-    float* dp;
-    CHK(out_ptr(c, probs, c0 * k, cnt * k, dev, S_OUT0, &dp));
-    CHK(run_si_net(c, dx, cnt, dp, nullptr, nullptr));
-    CHK(copy_back(c, probs, c0 * k, dp, cnt * k, dev));
-    if (!dev) HIPCHK(c, hipStreamSynchronize(c->stream));
-  }
+  CHK(for_microbatches(c, false, n, [&](int64_t c0, int64_t cnt) -> int {
+    return guarded(c, dev, c->si_f32_only, [&]() -> int {
+      const float* dx = x + c0 * SI_T * SI_D;
+      if (!dev) {
+        void* p = nullptr;
+        CHK(ws_get(c, S_IN, cnt * SI_T * SI_D * sizeof(float), &p));
+        HIPCHK(c, hipMemcpyAsync(p, dx, cnt * SI_T * SI_D * sizeof(float), hipMemcpyHostToDevice,
+                                 c->stream));
+        dx = static_cast<float*>(p);
+      }
+      float* dp;
+      CHK(out_ptr(c, probs, c0 * k, cnt * k, dev, S_OUT0, &dp));
+      CHK(run_si_net(c, dx, cnt, dp, nullptr, nullptr));
+      CHK(copy_back(c, probs, c0 * k, dp, cnt * k, dev));
+      if (!dev) HIPCHK(c, hipStreamSynchronize(c->stream));
+      return MMLA_OK;
+    });
+  }));
   return finish(c, dev);
 }
 
 int mmla_od_pipeline(mmla_ctx* c, const int16_t* pcm, int64_t n, int64_t stride,
                      const int32_t* lens, int32_t clip_len, float* probs, int32_t* argmax,
-                     uint32_t flags) {
+                     uint8_t* silent, uint32_t flags) {
   if (!c) return MMLA_E_INVALID;
   if (bad_pcm_args(pcm, n, stride, lens, clip_len)) return fail(c, MMLA_E_INVALID, "bad pcm args");
   if (!c->od_loaded) return fail(c, MMLA_E_NOWEIGHTS, "OD weights not loaded");
   HIPCHK(c, hipSetDevice(c->device));
   const bool dev = flags & MMLA_DEVICE_PTR;
-  for (int64_t c0 = 0; c0 < n; c0 += c->od_mb) {
-    const int64_t cnt = std::min(c->od_mb, n - c0);
-    Pcm p;
-    CHK(stage_pcm(c, pcm, c0, cnt, stride, lens, clip_len, MMLA_OD_CLIP, dev, &p));
-    void* pimg = nullptr;
-    CHK(ws_get(c, S_IMG, cnt * OD_IMG, &pimg));
-    OdFeArgs a{};
-    a.pcm = p.p;
-    a.clip_stride = p.stride;
-    a.lens = p.lens;
-    a.clip_len = p.clip_len;
-    a.tables = c->od_tables;
-    a.img = static_cast<uint8_t*>(pimg);
-    void* ps = nullptr;
-    CHK(ws_get(c, S_FESCR, (size_t)cnt * OD_PIX * sizeof(float), &ps));
-    a.scratch = static_cast<float*>(ps);
-    LAUNCH(c, MMLA_STAGE_OD_FE, od_fe_bytes(cnt, a), od_fe_launch(a, cnt, c->stream));
-    float* dp;
-    int32_t* da;
-    CHK(out_ptr(c, probs, c0 * 2, cnt * 2, dev, S_OUT0, &dp));
-    CHK(out_ptr(c, argmax, c0, cnt, dev, S_OUT1, &da));
-    CHK(run_od_net(c, a.img, nullptr, cnt, dp, da));
-    CHK(copy_back(c, probs, c0 * 2, dp, cnt * 2, dev));
-    CHK(copy_back(c, argmax, c0, da, cnt, dev));
-    if (!dev) HIPCHK(c, hipStreamSynchronize(c->stream));
-  }
+  CHK(for_microbatches(c, true, n, [&](int64_t c0, int64_t cnt) -> int {
+    return guarded(c, dev, c->od_f32_only, [&]() -> int {
+      Pcm p;
+      CHK(stage_pcm(c, pcm, c0, cnt, stride, lens, clip_len, MMLA_OD_CLIP, dev, &p));
+      void* pimg = nullptr;
+      CHK(ws_get(c, S_IMG, cnt * OD_IMG, &pimg));
+      OdFeArgs a{};
+      a.pcm = p.p;
+      a.clip_stride = p.stride;
+      a.lens = p.lens;
+      a.clip_len = p.clip_len;
+      a.tables = c->od_tables;
+      a.img = static_cast<uint8_t*>(pimg);
+      void* ps = nullptr;
+      CHK(ws_get(c, S_FESCR, (size_t)cnt * OD_PIX * sizeof(float), &ps));
+      a.scratch = static_cast<float*>(ps);
+      LAUNCH(c, MMLA_STAGE_OD_FE, od_fe_bytes(cnt, a), od_fe_launch(a, cnt, c->stream));
+      float* dp;
+      int32_t* da;
+      uint8_t* ds;
+      CHK(out_ptr(c, probs, c0 * 2, cnt * 2, dev, S_OUT0, &dp));
+      CHK(out_ptr(c, argmax, c0, cnt, dev, S_OUT1, &da));
+      CHK(out_ptr(c, silent, c0, cnt, dev, S_OUT2, &ds));
+      OdGate g;
+      g.lens = p.lens;
+      g.clip_len = lens ? 0 : clip_len;   // the true length decides, not the staged width
+      g.silent = ds;
+      CHK(run_od_net(c, a.img, nullptr, cnt, dp, da, g));
+      CHK(copy_back(c, probs, c0 * 2, dp, cnt * 2, dev));
+      CHK(copy_back(c, argmax, c0, da, cnt, dev));
+      CHK(copy_back(c, silent, c0, ds, cnt, dev));
+      if (!dev) HIPCHK(c, hipStreamSynchronize(c->stream));
+      return MMLA_OK;
+    });
+  }));
   return finish(c, dev);
 }
 
@@ -1233,37 +1436,39 @@ int mmla_si_pipeline(mmla_ctx* c, const int16_t* pcm, int64_t n, int64_t stride,
   HIPCHK(c, hipSetDevice(c->device));
   const bool dev = flags & MMLA_DEVICE_PTR;
   const int k = c->si.k;
-  for (int64_t c0 = 0; c0 < n; c0 += c->si_mb) {
-    const int64_t cnt = std::min(c->si_mb, n - c0);
-    Pcm p;
-    CHK(stage_pcm(c, pcm, c0, cnt, stride, lens, clip_len, SI_NEED_SAMPLES, dev, &p));
-    void *pf, *ps;
-    CHK(ws_get(c, S_FEAT, cnt * SI_T * SI_D * sizeof(float), &pf));
-    CHK(ws_get(c, S_SILENT, cnt, &ps));
-    SiFeArgs a{};
-    a.pcm = p.p;
-    a.clip_stride = p.stride;
-    a.lens = p.lens;
-    a.clip_len = lens ? 0 : clip_len;
-    a.tables = c->si_tables;
-    a.feat = static_cast<float*>(pf);
-    a.silent = static_cast<uint8_t*>(ps);
-    LAUNCH(c, MMLA_STAGE_SI_FE, si_fe_bytes(cnt, a), si_fe_launch(a, cnt, c->stream));
-    float* dp;
-    int32_t* da;
-    CHK(out_ptr(c, probs, c0 * k, cnt * k, dev, S_OUT0, &dp));
-    CHK(out_ptr(c, argmax, c0, cnt, dev, S_OUT1, &da));
-    CHK(run_si_net(c, a.feat, cnt, dp, da, a.silent));
-    CHK(copy_back(c, probs, c0 * k, dp, cnt * k, dev));
-    CHK(copy_back(c, argmax, c0, da, cnt, dev));
-    if (silent) {
-      if (dev)
-        HIPCHK(c, hipMemcpyAsync(silent + c0, a.silent, cnt, hipMemcpyDeviceToDevice, c->stream));
-      else
-        HIPCHK(c, hipMemcpyAsync(silent + c0, a.silent, cnt, hipMemcpyDeviceToHost, c->stream));
-    }
-    if (!dev) HIPCHK(c, hipStreamSynchronize(c->stream));
-  }
+  CHK(for_microbatches(c, false, n, [&](int64_t c0, int64_t cnt) -> int {
+    return guarded(c, dev, c->si_f32_only, [&]() -> int {
+      Pcm p;
+      CHK(stage_pcm(c, pcm, c0, cnt, stride, lens, clip_len, SI_NEED_SAMPLES, dev, &p));
+      void *pf, *ps;
+      CHK(ws_get(c, S_FEAT, cnt * SI_T * SI_D * sizeof(float), &pf));
+      CHK(ws_get(c, S_SILENT, cnt, &ps));
+      SiFeArgs a{};
+      a.pcm = p.p;
+      a.clip_stride = p.stride;
+      a.lens = p.lens;
+      a.clip_len = lens ? 0 : clip_len;
+      a.tables = c->si_tables;
+      a.feat = static_cast<float*>(pf);
+      a.silent = static_cast<uint8_t*>(ps);
+      LAUNCH(c, MMLA_STAGE_SI_FE, si_fe_bytes(cnt, a), si_fe_launch(a, cnt, c->stream));
+      float* dp;
+      int32_t* da;
+      CHK(out_ptr(c, probs, c0 * k, cnt * k, dev, S_OUT0, &dp));
+      CHK(out_ptr(c, argmax, c0, cnt, dev, S_OUT1, &da));
+      CHK(run_si_net(c, a.feat, cnt, dp, da, a.silent));
+      CHK(copy_back(c, probs, c0 * k, dp, cnt * k, dev));
+      CHK(copy_back(c, argmax, c0, da, cnt, dev));
+      if (silent) {
+        if (dev)
+          HIPCHK(c, hipMemcpyAsync(silent + c0, a.silent, cnt, hipMemcpyDeviceToDevice, c->stream));
+        else
+          HIPCHK(c, hipMemcpyAsync(silent + c0, a.silent, cnt, hipMemcpyDeviceToHost, c->stream));
+      }
+      if (!dev) HIPCHK(c, hipStreamSynchronize(c->stream));
+      return MMLA_OK;
+    });
+  }));
   return finish(c, dev);
 }
 
@@ -1277,7 +1482,8 @@ int mmla_debug_od_trace(mmla_ctx* c, const float* x, int64_t n, int stage, float
   HIPCHK(c, hipMemcpyAsync(p, x, n * OD_IMG * sizeof(float), hipMemcpyHostToDevice, c->stream));
   const float* tap = nullptr;
   int64_t tn = 0;
-  CHK(run_od_net(c, nullptr, static_cast<float*>(p), n, nullptr, nullptr, stage, &tap, &tn));
+  CHK(run_od_net(c, nullptr, static_cast<float*>(p), n, nullptr, nullptr, OdGate(), stage, &tap,
+                 &tn));
   if (tn > out_floats) return fail(c, MMLA_E_SHAPE, "trace stage %d needs %lld floats", stage, (long long)tn);
   HIPCHK(c, hipMemcpyAsync(out, tap, tn * sizeof(float), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));

@@ -20,6 +20,7 @@ struct ConvH3Args {
   int pro, epi, pool_out;
   int pool_in;           // Conv1D only: x is [N, h_in, 1, Cin] and the conv reads MaxPool1D(2, same) of it
   int h_in;
+  int* range_flag;       // nullable: set to 1 when a staged operand is >= 65504 in magnitude / inf
 };
 
 // Picks the tile and launches; returns hipErrorInvalidValue for unsupported shapes.

@@ -37,6 +37,7 @@ constexpr int NT = 256;
 constexpr int BM = 128;
 constexpr float LO_SCALE = 2048.0f;
 constexpr float LO_INV = 1.0f / 2048.0f;
+constexpr float F16_RANGE = 65504.0f;   // largest finite fp16
 
 template <int PRO>
 MMLA_DEV float pro_fn(float v, float sc, float sh) {
@@ -173,6 +174,7 @@ __global__ void __launch_bounds__(NT, 2) conv_h3_kernel(ConvH3Args a) {
   }
   const float* xclip = a.x + clip * HH * a.w * a.cin;
 
+  bool rbad = false;   // 3xFP16 range guard: a staged operand left the fp16 range
   const int nchunks = a.cin_pad / CK;
   for (int ch = 0; ch < nchunks; ++ch) {
     const int ci0 = ch * CK;
@@ -259,6 +261,7 @@ __global__ void __launch_bounds__(NT, 2) conv_h3_kernel(ConvH3Args a) {
           v.w = pro_fn<PRO>(v.w, sc.w, sh.w);
         }
       }
+      rbad |= !(fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))) < F16_RANGE);
       f16x4 hv, lv;
       hv[0] = (_Float16)v.x;
       hv[1] = (_Float16)v.y;
@@ -429,6 +432,7 @@ __global__ void __launch_bounds__(NT, 2) conv_h3_kernel(ConvH3Args a) {
       }
     }
   }
+  if (rbad && a.range_flag) *a.range_flag = 1;
 }
 
 template <int KH, int KW, int CK, int BN, int TW, int PRO, int EPI, bool POOL, bool V4 = true,

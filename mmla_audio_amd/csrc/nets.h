@@ -24,11 +24,17 @@ hipError_t bilstm_launch(const float* seq, int n, int T, int D, const float* wca
 // accumulation); w*h / w*l = bilstm_h3_split_weights(wcat): [1024][256 + D] fp16 bits.
 hipError_t bilstm_h3_launch(const float* seq, int n, int T, int D, const uint16_t* wfh,
                             const uint16_t* wfl, const uint16_t* wbh, const uint16_t* wbl,
-                            const float* bias_fwd, const float* bias_bwd, float* out, hipStream_t s);
+                            const float* bias_fwd, const float* bias_bwd, float* out,
+                            int* range_flag /*nullable: set when |x| >= 65504 / 64*/, hipStream_t s);
 void bilstm_h3_split_weights(const float* wcat, int D, uint16_t* hi, uint16_t* lo);
-// OD head: LeakyReLU(0.3) -> Dense(512 -> 2) -> softmax; probs [n,2], argmax [n] (nullable)
+// The kernel scales the weights by 2^8 before the fp16 split: false when max |w| * 256 >= 65504.
+bool bilstm_h3_weights_in_range(const float* wcat, int D);
+// OD head: LeakyReLU(0.3) -> Dense(512 -> 2) -> softmax; probs [n,2], argmax [n] (nullable).
+// The 'silent' gate of record_on_pc.py:141-154: with clip_len >= 0, clips with fewer than 4000
+// samples (lens[i], or clip_len when lens is null) get argmax -1 and silent[i] = 1 (nullable).
 hipError_t od_head_launch(const float* h, int n, const float* w /*[512][2]*/, const float* b,
-                          float* probs, int32_t* argmax, hipStream_t s);
+                          float* probs, int32_t* argmax, const int32_t* lens, int clip_len,
+                          uint8_t* silent, hipStream_t s);
 // SI head activation on logits [n, ld]: softmax (head 0) or sigmoid (head 1) over the first k;
 // argmax [n] (-1 where silent[i] != 0).
 hipError_t si_head_launch(const float* logits, int n, int k, int ld, int head, float* probs,

@@ -210,7 +210,8 @@ __global__ void __launch_bounds__(512) bilstm_h3_kernel(const float* __restrict_
                                                         const uint16_t* __restrict__ wbl,
                                                         const float* __restrict__ bf,
                                                         const float* __restrict__ bb,
-                                                        float* __restrict__ out) {
+                                                        float* __restrict__ out,
+                                                        int* __restrict__ range_flag) {
   constexpr int K = LSTM_U + D;          // 384
   constexpr int KST = K / 16;            // k-steps
   constexpr int LDA = K + 8;             // fp16 per A row (16-B pad)
@@ -244,6 +245,7 @@ __global__ void __launch_bounds__(512) bilstm_h3_kernel(const float* __restrict_
 #pragma unroll
     for (int r = 0; r < 16; ++r) cst[mt][r] = 0.0f;
 
+  bool rbad = false;   // 3xFP16 range guard: |x * 2^6| must stay below 65504 (|h| < 1 always)
   for (int s = 0; s < T; ++s) {
     const int t = dir == 0 ? s : T - 1 - s;
     // x_t -> A[:, 256:256+D] (float4 loads, split once)
@@ -252,6 +254,8 @@ __global__ void __launch_bounds__(512) bilstm_h3_kernel(const float* __restrict_
       const int64_t clip = c0 + r;
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
       if (clip < n) v = *reinterpret_cast<const float4*>(seq + (clip * T + t) * D + 4 * d4);
+      rbad |= !(fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))) <
+                65504.0f / LSTM_AS);
       _Float16 h0, h1, h2, h3, l0, l1, l2, l3;
       split1(v.x, h0, l0);
       split1(v.y, h1, l1);
@@ -338,11 +342,13 @@ __global__ void __launch_bounds__(512) bilstm_h3_kernel(const float* __restrict_
         Alo[row * LDA + col] = hl;
       }
   }
+  if (rbad && range_flag) *range_flag = 1;
 }
 
 __global__ void od_head_kernel(const float* __restrict__ h, int n, const float* __restrict__ w,
                                const float* __restrict__ b, float* __restrict__ probs,
-                               int32_t* __restrict__ argmax) {
+                               int32_t* __restrict__ argmax, const int32_t* __restrict__ lens,
+                               int clip_len, uint8_t* __restrict__ silent) {
   // one wave per clip
   const int lane = threadIdx.x & 63;
   const int64_t clip = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -365,7 +371,10 @@ __global__ void od_head_kernel(const float* __restrict__ h, int n, const float* 
       probs[clip * 2 + 0] = e0 / s;
       probs[clip * 2 + 1] = e1 / s;
     }
-    if (argmax) argmax[clip] = e1 / s > e0 / s ? 1 : 0;
+    // record_on_pc.py:141-154: fewer than 4000 samples (after VAD) -> 'silent', no class
+    const bool sil = clip_len >= 0 && (lens ? lens[clip] : clip_len) < 4000;
+    if (silent) silent[clip] = sil ? 1 : 0;
+    if (argmax) argmax[clip] = sil ? -1 : (e1 / s > e0 / s ? 1 : 0);
   }
 }
 
@@ -457,14 +466,21 @@ hipError_t bilstm_launch(const float* seq, int n, int T, int D, const float* wf,
 
 hipError_t bilstm_h3_launch(const float* seq, int n, int T, int D, const uint16_t* wfh,
                             const uint16_t* wfl, const uint16_t* wbh, const uint16_t* wbl,
-                            const float* bf, const float* bb, float* out, hipStream_t s) {
+                            const float* bf, const float* bb, float* out, int* range_flag,
+                            hipStream_t s) {
   if (n <= 0) return hipSuccess;
   if (D != 128) return hipErrorInvalidValue;
   // (MT 2 -- 64 clips per workgroup, half the weight stream per clip -- needs ~290 registers per
   // lane: spills at two waves per SIMD, so one 32-clip tile)
   hipLaunchKernelGGL((bilstm_h3_kernel<128, 1>), dim3(blocks_for(n, LSTM_ROWS), 2), dim3(512), 0, s,
-                     seq, n, T, wfh, wfl, wbh, wbl, bf, bb, out);
+                     seq, n, T, wfh, wfl, wbh, wbl, bf, bb, out, range_flag);
   return hipGetLastError();
+}
+
+bool bilstm_h3_weights_in_range(const float* wcat, int D) {
+  for (size_t i = 0; i < (size_t)(256 + D) * 1024; ++i)
+    if (!(fabsf(wcat[i]) * LSTM_WS < 65504.0f)) return false;   // also inf / NaN
+  return true;
 }
 
 void bilstm_h3_split_weights(const float* wcat, int D, uint16_t* hi, uint16_t* lo) {
@@ -480,10 +496,11 @@ void bilstm_h3_split_weights(const float* wcat, int D, uint16_t* hi, uint16_t* l
 }
 
 hipError_t od_head_launch(const float* h, int n, const float* w, const float* b, float* probs,
-                          int32_t* argmax, hipStream_t s) {
+                          int32_t* argmax, const int32_t* lens, int clip_len, uint8_t* silent,
+                          hipStream_t s) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(od_head_kernel, dim3(blocks_for((int64_t)n * 64, 256)), dim3(256), 0, s, h, n,
-                     w, b, probs, argmax);
+                     w, b, probs, argmax, lens, clip_len, silent);
   return hipGetLastError();
 }
 

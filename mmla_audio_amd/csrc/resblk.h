@@ -26,6 +26,7 @@ struct ResBlkArgs {
   float* y;                // non-pool: [N, H, W, C] = x + conv;  pool: [N, ceil(H/2), ceil(W/2), C]
   int n, h, w;             //   = MaxPool2D(2, 'same')(conv) + Conv2D(1x1, stride 2)(x)
   int tiles_h, tiles_w;    // set by resblk_launch
+  int* range_flag;         // nullable: set to 1 when an operand split into fp16 is >= 65504 / inf
 };
 
 // K of the 3x3 conv padded to the MFMA k-step (32).

@@ -72,6 +72,11 @@ __device__ __forceinline__ void split2(f32x2 v, f16x2& h, f16x2& l) {
 }
 
 // the 3 channels of image pixel `pix` (uint8 decoded PNG or float NHWC), as floats
+// 3xFP16 range guard: false when a value about to be split is >= 65504 in magnitude (or inf)
+__device__ __forceinline__ bool in_f16_range(f32x2 a, f32x2 b) {
+  return fmaxf(fmaxf(fabsf(a.x), fabsf(a.y)), fmaxf(fabsf(b.x), fabsf(b.y))) < 65504.0f;
+}
+
 __device__ __forceinline__ float4 image_px(const ResBlkArgs& a, int64_t pix) {
   if (a.img8) {
     const uint8_t* p = a.img8 + pix * 3;
@@ -153,6 +158,7 @@ __global__ void __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(R
   const int h0 = th_i * TH, w0 = (tile - th_i * a.tiles_w) * TW;
 
   RB_MARK(0);
+  bool rbad = false;   // 3xFP16 range guard (ResBlkArgs::range_flag)
   // ---- per-thread parameters first: BN1 (+ stem) for the staging, BN2 / bias for the t1 re-staging
   //      and the epilogue.  Issued here they share the halo's memory latency; issued where they are
   //      used (after a barrier or a dependent wait) each group cost a round trip of its own --------
@@ -295,6 +301,7 @@ __global__ void __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(R
       const f32x2 u01 = elu2(v01 * sc01 + sh01), u23 = elu2(v23 * sc23 + sh23);
       v01 = ok ? u01 : f32x2{0.f, 0.f};
       v23 = ok ? u23 : f32x2{0.f, 0.f};
+      rbad |= !in_f16_range(v01, v23);
       f16x2 h01, l01, h23, l23;
       split2(v01, h01, l01);
       split2(v23, h23, l23);
@@ -319,6 +326,8 @@ __global__ void __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(R
 #pragma unroll
       for (int j = 0; j < MSC; ++j) {
         const float4 u0 = scx[s][j][0], u1 = scx[s][j][1];
+        rbad |= !in_f16_range(f32x2{u0.x, u0.y}, f32x2{u0.z, u0.w}) ||
+                !in_f16_range(f32x2{u1.x, u1.y}, f32x2{u1.z, u1.w});
         f16x2 h0_, l0_, h1_, l1_, h2_, l2_, h3_, l3_;
         split2(f32x2{u0.x, u0.y}, h0_, l0_);
         split2(f32x2{u0.z, u0.w}, h1_, l1_);
@@ -417,7 +426,11 @@ __global__ void __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(R
 #endif
           const f32x2 x1 = {acc1[m][nt][i], acc1[m][nt][i + 1]};
           const f32x2 x2 = {acc2[m][nt][i], acc2[m][nt][i + 1]};
-          const f32x2 v = elu2(x1 * s2v + (x2 * s2l + c2v)) * rmask;
+          const f32x2 u = elu2(x1 * s2v + (x2 * s2l + c2v));
+          // guard only the live t1 rows: the padding rows (>= TR, and outside the image) hold
+          // whatever GEMM 1 made of unstaged LDS and are multiplied by 0 / never read
+          rbad |= rm != 0.0f && wm * MT1 + m < G::TR && !in_f16_range(u, u);
+          const f32x2 v = u * rmask;
           f16x2 hv, lv;
           split2(v, hv, lv);
           thb[(m * TW + i) * TPS + n] = hv.x;
@@ -550,6 +563,7 @@ __global__ void __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(R
     }
   }
   RB_MARK(7);
+  if (rbad && a.range_flag) *a.range_flag = 1;
 }
 
 template <int CIN, int C, bool POOL, bool STEM = false>

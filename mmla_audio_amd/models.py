@@ -64,7 +64,8 @@ class OverlapDetectionModel(_Model):
         return self.ctx.od_forward(x)
 
     def predict_wavs(self, pcm, lens=None):
-        """Fused WAV -> class (no PNG round trip): int16 [N, L] -> (probs [N,2], argmax [N])."""
+        """Fused WAV -> class (no PNG round trip): int16 [N, L] -> (probs [N,2], argmax [N]
+        (-1 = 'silent', fewer than 4000 samples: record_on_pc.py:141-154), silent [N])."""
         self._ensure_loaded()
         return self.ctx.od_pipeline(pcm, lens)
 

@@ -43,7 +43,7 @@ def test_shim_signatures_cover_header():
 
 
 def test_abi_version(lib):
-    assert lib.mmla_abi_version() == 1
+    assert lib.mmla_abi_version() == 2
 
 
 def test_null_args_rejected_without_device(lib):

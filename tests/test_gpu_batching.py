@@ -24,18 +24,18 @@ def ctx():
 
 def test_od_batch_invariance(ctx):
     pcm = synth.batch(800, 37, 40000)
-    p_all, a_all = ctx.od_pipeline(pcm)
+    p_all, a_all, _ = ctx.od_pipeline(pcm)
     for i in (0, 17, 36):
-        p1, a1 = ctx.od_pipeline(pcm[i:i + 1])
+        p1, a1, _ = ctx.od_pipeline(pcm[i:i + 1])
         assert np.array_equal(p1[0], p_all[i]) and a1[0] == a_all[i]
 
 
 def test_od_microbatch_boundaries(ctx):
     pcm = synth.batch(900, 150, 40000)
-    p_ref, a_ref = ctx.od_pipeline(pcm)
+    p_ref, a_ref, _ = ctx.od_pipeline(pcm)
     ctx.set_microbatch(64, 0)            # 150 clips -> 64 + 64 + 22
     try:
-        p, a = ctx.od_pipeline(pcm)
+        p, a, _ = ctx.od_pipeline(pcm)
         f = ctx.od_features(pcm[:70], db=False, zcr=False)
         x = ctx.od_forward(f['img'])
     finally:
@@ -57,9 +57,25 @@ def test_si_microbatch_boundaries(ctx):
 
 
 def test_empty_batches(ctx):
-    p, a = ctx.od_pipeline(np.zeros((0, 40000), np.int16))
+    p, a, _ = ctx.od_pipeline(np.zeros((0, 40000), np.int16))
     assert p.shape == (0, 2) and a.shape == (0,)
     f = ctx.od_features(np.zeros((0, 40000), np.int16))
     assert f['norm'].shape == (0, 128, 151)
     x = ctx.od_forward(np.zeros((0, 128, 151, 3), np.float32))
     assert x.shape == (0, 2)
+
+
+def test_od_silent_gate(ctx):
+    """record_on_pc.py:141-154: fewer than 4000 samples -> 'silent' (argmax -1), others classify
+    exactly as they do alone."""
+    lens = [3999, 4000, 40000, 0, 100, 23999]
+    pcm = [synth.clip(1500 + i, n) for i, n in enumerate(lens)]
+    p, a, s = ctx.od_pipeline(pcm)
+    assert s.tolist() == [True, False, False, True, True, False]
+    assert all(a[i] == -1 for i in (0, 3, 4))
+    for i in (1, 2, 5):
+        p1, a1, s1 = ctx.od_pipeline(pcm[i][None])
+        assert not s1[0] and a1[0] == a[i] and np.array_equal(p1[0], p[i])
+    # without lens the clip length decides for every clip
+    _, a2, s2 = ctx.od_pipeline(np.zeros((3, 3000), np.int16))
+    assert s2.all() and (a2 == -1).all()

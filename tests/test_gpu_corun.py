@@ -1,6 +1,10 @@
 """Timing independence: the OD and SI pipelines give bit-identical results whether they run alone
 or while a second context's kernels co-run on another stream (a kernel with a missing barrier or
-an unordered LDS/global dependency would drift under the changed co-residency)."""
+an unordered LDS/global dependency would drift under the changed co-residency).
+
+Both contexts' work is enqueued back to back with no host synchronisation in between; events on the
+two streams show that context b's first kernel was eligible to start before context a finished.
+"""
 import numpy as np
 import pytest
 
@@ -9,37 +13,47 @@ from oracle import synth
 pytestmark = pytest.mark.gpu
 
 
-def _ctx(seed):
+def _ctx(seed, stream):
     from mmla_audio_amd import _lib, weights
     c = _lib.Context(0)
     c.load_weights(weights.OD, weights.pack(weights.OD, weights.synthetic(weights.OD, seed=seed)), 2)
     Ws = weights.synthetic(weights.SI, seed=seed + 1, n_classes=8)
     c.load_weights(weights.SI, weights.pack(weights.SI, Ws, 8), 8, 1)
-    c.set_microbatch(64, 64)
+    c.set_microbatch(128, 128)
+    c.set_stream(stream.cuda_stream)
     return c
 
 
 def test_corun_bit_identical():
     import torch
-    a, b = _ctx(41), _ctx(41)
-    n = 256
+    sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+    a, b = _ctx(41, sa), _ctx(41, sb)
+    n = 1024
     od = torch.from_numpy(synth.batch(990, n, 40000)).cuda()
     si = torch.from_numpy(synth.batch(991, n, 24000)).cuda()
+    outs = {k: (torch.zeros((n, 2), device='cuda'), torch.zeros((n, 8), device='cuda'))
+            for k in ('solo', 'a', 'b')}
 
-    def run(c):
-        po = torch.zeros((n, 2), dtype=torch.float32, device='cuda')
-        ps = torch.zeros((n, 8), dtype=torch.float32, device='cuda')
-        torch.cuda.synchronize()
-        c.od_pipeline_dev(od.data_ptr(), n, 40000, 40000, po.data_ptr(), 0)
-        c.si_pipeline_dev(si.data_ptr(), n, 24000, 24000, ps.data_ptr(), 0)
-        return po, ps
+    def enqueue(c, po, ps):
+        c.od_pipeline_dev(od.data_ptr(), n, 40000, 40000, po.data_ptr())
+        c.si_pipeline_dev(si.data_ptr(), n, 24000, 24000, ps.data_ptr())
 
-    ro, rs = run(a)
     torch.cuda.synchronize()
-    ro, rs = ro.cpu().numpy(), rs.cpu().numpy()
+    enqueue(a, *outs['solo'])
+    torch.cuda.synchronize()
+    ro, rs = (t.cpu().numpy() for t in outs['solo'])
     for _ in range(3):
-        (ao, as_), (bo, bs) = run(a), run(b)   # both contexts' streams busy at once
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+        ev[0].record(sa)
+        enqueue(a, *outs['a'])
+        ev[1].record(sa)
+        ev[2].record(sb)
+        enqueue(b, *outs['b'])        # no synchronisation between the two contexts
+        ev[3].record(sb)
         torch.cuda.synchronize()
-        for o, s_ in ((ao, as_), (bo, bs)):
-            assert np.array_equal(o.cpu().numpy(), ro)
-            assert np.array_equal(s_.cpu().numpy(), rs)
+        a_end = ev[0].elapsed_time(ev[1])
+        b_start = ev[0].elapsed_time(ev[2])
+        assert b_start < a_end, f'b eligible at {b_start:.2f} ms, a ran until {a_end:.2f} ms'
+        for k in ('a', 'b'):
+            assert np.array_equal(outs[k][0].cpu().numpy(), ro)
+            assert np.array_equal(outs[k][1].cpu().numpy(), rs)

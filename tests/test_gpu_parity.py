@@ -141,7 +141,7 @@ def test_od_pipeline_matches_features_then_forward(ctx):
     W = weights.synthetic(weights.OD, seed=4)
     ctx.load_weights(weights.OD, weights.pack(weights.OD, W), 2)
     pcm = synth.batch(500, 12, 40000)
-    probs, am = ctx.od_pipeline(pcm)
+    probs, am, _ = ctx.od_pipeline(pcm)
     f = ctx.od_features(pcm, db=False, norm=False, zcr=False)
     p2 = ctx.od_forward(f['img'])
     assert np.array_equal(probs, p2)
@@ -178,7 +178,7 @@ def test_device_pointer_mode_matches_host(ctx):
     W = weights.synthetic(weights.OD, seed=7)
     ctx.load_weights(weights.OD, weights.pack(weights.OD, W), 2)
     pcm = synth.batch(700, 6, 40000)
-    ph, ah = ctx.od_pipeline(pcm)
+    ph, ah, _ = ctx.od_pipeline(pcm)
     d_pcm = torch.from_numpy(pcm).cuda()
     d_p = torch.empty((6, 2), dtype=torch.float32, device='cuda')
     d_a = torch.empty(6, dtype=torch.int32, device='cuda')

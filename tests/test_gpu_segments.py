@@ -29,7 +29,7 @@ def test_predict_segments_matches_per_window(model, seconds, step):
     if n == 0:
         return
     windows = np.stack([sig[j * st: j * st + win] for j in range(n)])
-    p2, am2 = model.predict_wavs(windows)
+    p2, am2, _ = model.predict_wavs(windows)
     assert np.array_equal(probs, p2)
     assert np.array_equal(am, am2)
     assert labels == [odpp.OVERLAP_DEGREE[str(k)] for k in am2]

@@ -31,7 +31,7 @@ def test_od_guards(gctx, mb, n):
     gctx.set_microbatch(mb, 0)
     try:
         gctx.od_features(pcm)
-        p, a = gctx.od_pipeline(pcm)
+        p, a, _ = gctx.od_pipeline(pcm)
     finally:
         gctx.set_microbatch(0, 0)
     assert np.isfinite(p).all()
