@@ -5,9 +5,11 @@ Replaces ``tf.keras.models.load_model`` + ``Model.predict`` at the reference cal
 ``speaker_identification_post_processing.py:206,272``; ``overlap_detection_post_processing.py``).
 
 Weights: if ``<path>/variables/variables.data-00000-of-00001`` exists the trained tensors are read
-from the TF bundle (``tfbundle.load_bundle``); the reference does not ship that file
-(``.MISSING_LARGE_BLOBS``), so otherwise seeded synthetic weights in the exact reference layout are
-used and ``model.synthetic`` is True.
+from the TF bundle (``tfbundle.load_bundle``).  The reference does not ship that file
+(``.MISSING_LARGE_BLOBS``); like ``tf.keras.models.load_model`` on an incomplete SavedModel, loading
+then raises -- a drop-in must not log confident labels from a random net.  Seeded synthetic
+weights in the exact reference layout are used only on request (``allow_synthetic=True``;
+``model.synthetic`` is then True).
 """
 import os
 import warnings
@@ -91,15 +93,22 @@ class SpeakerIdModel(_Model):
         return self.ctx.si_pipeline(pcm, lens)
 
 
-def load_model(path, kind=None, n_classes=None, head=None, seed=0, device=None):
-    """tf.keras.models.load_model drop-in for the two reference model directories."""
+def load_model(path, kind=None, n_classes=None, head=None, seed=0, device=None,
+               allow_synthetic=False):
+    """tf.keras.models.load_model drop-in for the two reference model directories.  Raises
+    FileNotFoundError when the trained variables are absent, unless allow_synthetic=True."""
     kind = _kind_from_path(path) if kind is None else kind
     synthetic = False
     try:
         W = tfbundle.load_bundle(path, 40 if kind == weights.OD else 41)
         if kind == weights.SI:
             n_classes = W['layer_with_weights-42/kernel'].shape[1]
-    except (FileNotFoundError, OSError):
+    except (FileNotFoundError, OSError) as e:
+        if not allow_synthetic:
+            raise FileNotFoundError(
+                f'{path}: trained variables not found ({e}); the reference ships only '
+                f'variables.index (.MISSING_LARGE_BLOBS). Pass allow_synthetic=True for seeded '
+                f'synthetic weights in the reference layout.') from e
         warnings.warn(f'{path}: trained weights absent (reference .MISSING_LARGE_BLOBS); using seeded '
                       f'synthetic weights in the reference layout (seed={seed})')
         W = weights.synthetic(kind, seed=seed, n_classes=n_classes)

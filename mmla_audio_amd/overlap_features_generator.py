@@ -29,8 +29,18 @@ def _read_wav_int16(path):
 
 
 def write_png_rgba(path, rgb):
-    """Write an RGBA PNG (alpha 255) like ``plt.imsave`` does; decoders reading 3 channels
-    (``tf.image.decode_png(img, 3)``) get exactly ``rgb`` back."""
+    """Write the image file ``plt.imsave(path, img, origin="lower")`` writes (:151) for the already
+    flipped and quantised uint8 pixels ``rgb``: through matplotlib's own writer when it is
+    importable (uint8 RGB is written as is, alpha 255 -- the same bytes as the reference for the
+    same pixels and matplotlib version), else a minimal RGBA PNG encoder.  Either way decoders
+    reading 3 channels (``tf.image.decode_png(img, 3)``, record_on_pc.py:157) get ``rgb`` back."""
+    try:
+        from matplotlib import image as mimage
+    except ImportError:
+        mimage = None
+    if mimage is not None:
+        mimage.imsave(path, np.ascontiguousarray(rgb, dtype=np.uint8), origin='upper')
+        return
     h, w, _ = rgb.shape
     rgba = np.empty((h, w, 4), np.uint8)
     rgba[..., :3] = rgb

@@ -53,10 +53,31 @@ def input_feature_batch(pcm, lens=None, device=None):
     return _lib.default_context(device).si_features(pcm, lens=lens)
 
 
+_speakers_count_dict = {}   # the reference binarizer's mutable default argument: process-wide
+
+
+def binarizer(str_list, dim, speakers_count_dict=_speakers_count_dict):
+    """speaker_identification.py:122-138, same semantics: first-occurrence numbering that restarts
+    at 0 on every call while the dict (a mutable default argument) keeps the labels of earlier
+    calls -- so a new speaker in a later call can share an index with an old one, and an index
+    >= dim raises IndexError, exactly as in the reference."""
+    if not str_list:
+        raise UnboundLocalError("local variable 'result' referenced before assignment")
+    count = 0
+    rows = np.zeros((len(str_list), dim))
+    for i, s in enumerate(str_list):
+        if s not in speakers_count_dict:
+            speakers_count_dict[s] = count
+            count += 1
+        rows[i, speakers_count_dict[s]] = 1
+    return rows
+
+
 def make_feature_experiment(wav_files, device=None):
     """(:317-369): per file MFCC+deltas over the WHOLE file, zero-padded to a multiple of 256 frames
-    and cut into 256-frame windows; labels = file stem; returns (x, one-hot y, speaker_id dict).
-    Whole-file features are produced chunk-aligned on the GPU (see conversation_features)."""
+    and cut into 256-frame windows; labels = file stem; returns (x float64 [S,256,39], one-hot y,
+    speaker_id dict) with the reference's binarizer (state kept across calls).  Whole-file features
+    are produced chunk-aligned on the GPU (see conversation_features)."""
     train_x, train_y = [], []
     begin = time.time()
     for i, onewav in enumerate(wav_files):
@@ -68,13 +89,8 @@ def make_feature_experiment(wav_files, device=None):
         for c in chunks:
             train_x.append(c)
             train_y.append(label)
-    order = {}
-    for lab in train_y:
-        order.setdefault(lab, len(order))
-    y = np.zeros((len(train_y), len(order)))
-    for r, lab in enumerate(train_y):
-        y[r, order[lab]] = 1
-    speaker_id = {str(order[lab]): lab for lab in train_y}
+    y = binarizer(train_y, dim=len(set(train_y)))
+    speaker_id = {str(int(np.argmax(y[i]))): train_y[i] for i in range(len(train_y))}
     return np.asarray(train_x), y, speaker_id
 
 

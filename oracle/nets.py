@@ -23,6 +23,14 @@ CHANNELS = (32, 32, 32, 64, 64, 64, 128, 128, 128)
 POOL = (True, False, False, True, False, False, True, False, False)
 BN_EPS = 1e-3
 LEAKY_ALPHA = np.float32(0.3)
+OD_INPUT_SHAPE = (128, 151, 3)
+STEM_FILTERS = 16
+MEAN_AXIS = 1            # Lambda(lambda x: K.mean(x, axis=1)) on NHWC: the mel (H) axis
+LSTM_UNITS = 256
+OD_DROPOUT = 0.25        # before LeakyReLU; identity at inference
+OD_CLASSES = 2
+# tests/test_keras_graph.py checks these (and weights.od_spec's kernel shapes) layer by layer
+# against the graph in the reference's keras_metadata.pb (tests/golden/od_keras_graph.json)
 
 
 def _same_pad(n, k, s):
@@ -132,7 +140,7 @@ def od_forward(x, W, dtype=np.float64, return_logits=False):
             k += 4
         net = res + out
     assert k == 40
-    seq = net.mean(axis=1)                                   # Lambda(K.mean(x, axis=1)) -> [N,19,128]
+    seq = net.mean(axis=MEAN_AXIS)                           # Lambda(K.mean(x, axis=1)) -> [N,19,128]
     h = bilstm(seq, W, 40)
     h = np.where(h > 0, h, h * dtype(LEAKY_ALPHA))           # Dropout no-op, LeakyReLU(0.3)
     z = h @ W['layer_with_weights-41/kernel'].astype(dtype) + W['layer_with_weights-41/bias'].astype(dtype)

@@ -28,7 +28,13 @@ quantisation edge (tests allow that, see tests/test_oracle_golden.py).
   * the offline OD segmentation (overlap_detection_post_processing.py:23-85): segment count, names
     and the bytes of every segment WAV it writes, mono and stereo (seg_golden.npz).
 
-Output: tests/golden/od_golden.npz, si_golden.npz, seg_golden.npz (small, compressed).
+  * make_feature_experiment (speaker_identification.py:317-369): whole-file MFCC chunking, the
+    one-hot labels and speaker_id dict over two consecutive calls in one process -- its binarizer
+    keeps state in a mutable default argument (:122), so a second call numbers new speakers from 0
+    again (si_experiment_golden.npz).
+
+Output: tests/golden/od_golden.npz, si_golden.npz, seg_golden.npz, si_experiment_golden.npz
+(small, compressed).  ``python tests/golden/make_golden.py exp`` regenerates only the last.
 """
 import hashlib
 import io
@@ -208,7 +214,39 @@ def _segmentation_cases(ofg_mod, tmp):
     return seg
 
 
-def main():
+EXP_CALLS = [
+    # make_feature_experiment calls made one after the other in ONE process: the reference's
+    # binarizer keeps its speakers_count_dict (a mutable default argument) across calls
+    [('alice', 20, 51200), ('bob', 21, 16000), ('alice', 22, 8000)],
+    [('carol', 23, 30000), ('alice', 24, 12000)],
+]
+
+
+def _experiment_cases(si_mod, tmp):
+    """make_feature_experiment (speaker_identification.py:317-369) on synthetic speaker WAVs"""
+    exp = {}
+    for k, call in enumerate(EXP_CALLS):
+        d = os.path.join(tmp, f'exp{k}')
+        os.makedirs(d, exist_ok=True)
+        files = []
+        for j, (label, seed, n) in enumerate(call):
+            sub = os.path.join(d, str(j))       # same speaker twice: same stem, another directory
+            os.makedirs(sub, exist_ok=True)
+            path = os.path.join(sub, f'{label}.wav')
+            _write_wav(path, synth.clip(seed, n))
+            files.append(path)
+        x, y, spk = si_mod.make_feature_experiment(files)
+        exp[f'x_{k}'] = np.asarray(x, np.float64)
+        exp[f'y_{k}'] = np.asarray(y, np.float64)
+        exp[f'speaker_id_{k}'] = np.array(sorted(spk.items()))
+        exp[f'labels_{k}'] = np.array([c[0] for c in call])
+        exp[f'seeds_{k}'] = np.array([c[1] for c in call])
+        exp[f'lens_{k}'] = np.array([c[2] for c in call])
+        print('EXP', k, x.shape, y.shape, spk)
+    return exp
+
+
+def main(parts=('od', 'si', 'seg', 'exp')):
     _install_stubs()
     ofg_mod = _load_reference('OverlapDetection/scripts/overlap_features_generator.py', 'ref_ofg')
     si_mod = _load_reference('SpeakerIdentification/scripts/speaker_identification.py', 'ref_si')
@@ -216,6 +254,11 @@ def main():
     assert ofg.get_attributes() == (400, 160, 16000)
 
     tmp = tempfile.mkdtemp(prefix='mmla_golden_')
+    if 'exp' in parts:
+        np.savez_compressed(os.path.join(HERE, 'si_experiment_golden.npz'),
+                            **_experiment_cases(si_mod, tmp))
+    if not {'od', 'si', 'seg'} & set(parts):
+        return
     od = {'names': np.array([c[0] for c in OD_CASES])}
     for i, (name, gen) in enumerate(OD_CASES):
         pcm = gen()
@@ -259,4 +302,4 @@ def main():
 
 
 if __name__ == '__main__':
-    main()
+    main(tuple(sys.argv[1:]) or ('od', 'si', 'seg', 'exp'))
