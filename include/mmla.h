@@ -192,6 +192,33 @@ int mmla_nr_reduce(mmla_ctx* ctx, const float* y, int64_t n_signals, int64_t str
                    float* out, uint32_t flags);
 
 /*
+ * Silence removal, replaces save_wave_file(silence_remove=True) (OverlapDetection/scripts/
+ * record_on_pc.py:214-226, frame_generator :229-243, vad_collector :246-295; the same functions in
+ * SpeakerIdentification/scripts/record_on_pc.py:196 and speaker_identification_post_processing.py:
+ * 176-187,225-251).  Frames of 30 ms (480 samples) that END BEFORE the item's last sample,
+ * webrtcvad.Vad(mode).is_speech per frame (py-webrtcvad / WebRTC fixed-point VAD, 16 kHz path),
+ * the 10-frame ring-buffer trigger (> 90 % voiced / unvoiced), and the voiced frames written back
+ * in order: item i -> out + i * stride, out_lens[i] samples (a multiple of 480).
+ * mmla_vad_reset: (re)creates n_streams independent detectors in the context.  The reference keeps
+ * ONE module-level Vad(3) whose GMM state carries across clips; a stream is that object: its items
+ * are processed in order, and its state persists across calls until the next reset.
+ * mmla_vad_remove_silence: n_items = n_streams * items_per_stream; stream s owns items
+ * [s * items_per_stream, (s + 1) * items_per_stream).  speech [n_items][max_frames] u8 receives the
+ * per-frame decisions (nullable); max_frames 0 = the frames of the widest item.
+ * mmla_vad_collect: the collector and rewrite alone, on caller-supplied decisions `speech`.
+ * mmla_pcm16: sf.write(path, y, 16000) of float audio as PCM_16 (:212): (short) lrintf(y * 32767).
+ */
+int mmla_vad_reset(mmla_ctx* ctx, int64_t n_streams, int32_t mode);
+int mmla_vad_remove_silence(mmla_ctx* ctx, const int16_t* pcm, int64_t n_items, int64_t stride,
+                            const int32_t* lens, int32_t clip_len, int64_t items_per_stream,
+                            int16_t* out, int32_t* out_lens, uint8_t* speech, int32_t max_frames,
+                            uint32_t flags);
+int mmla_vad_collect(mmla_ctx* ctx, const int16_t* pcm, int64_t n_items, int64_t stride,
+                     const int32_t* lens, int32_t clip_len, const uint8_t* speech, int32_t max_frames,
+                     int16_t* out, int32_t* out_lens, uint32_t flags);
+int mmla_pcm16(mmla_ctx* ctx, const float* y, int64_t n, int16_t* out, uint32_t flags);
+
+/*
  * Kernel tracing (replaces the reference's time.time() prints, overlap_detector_run.py:49-104).
  * When enabled, every kernel launch is bracketed by hipEvents on the context stream and its device
  * time is accumulated per stage together with the stage's algorithmic work (bytes for the

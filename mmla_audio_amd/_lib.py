@@ -57,6 +57,10 @@ SIGNATURES = {
     'mmla_profile_enable': [_P, ctypes.c_int],
     'mmla_profile_read': [_P, _P, _P, _P, ctypes.c_int],
     'mmla_debug_od_trace': [_P, _P, _I64, ctypes.c_int, _P, _I64],
+    'mmla_vad_reset': [_P, _I64, _I32],
+    'mmla_vad_remove_silence': [_P, _P, _I64, _I64, _P, _I32, _I64, _P, _P, _P, _I32, _U32],
+    'mmla_vad_collect': [_P, _P, _I64, _I64, _P, _I32, _P, _I32, _P, _P, _U32],
+    'mmla_pcm16': [_P, _P, _I64, _P, _U32],
 }
 
 NSTAGES = 7
@@ -229,6 +233,50 @@ class Context:
     def nr_reduce_dev(self, y, n, stride, length, out):
         self._check(self.lib.mmla_nr_reduce(self.h, y, n, stride, length, out, MMLA_DEVICE_PTR),
                     'mmla_nr_reduce(dev)')
+
+    # -- silence removal -----------------------------------------------------
+    def vad_reset(self, n_streams=1, mode=3):
+        """n_streams fresh webrtcvad.Vad(mode) detectors (state kept in the context)."""
+        self._check(self.lib.mmla_vad_reset(self.h, int(n_streams), int(mode)), 'mmla_vad_reset')
+        self.vad_streams = int(n_streams)
+
+    def vad_remove_silence(self, pcm, lens=None, items_per_stream=1):
+        """save_wave_file(silence_remove=True) of every item: int16 [n, L] (or a list) ->
+        (voiced PCM list of int16 arrays, per-frame speech flags list).  Items of one stream are
+        consecutive and processed in order with that stream's detector state."""
+        a, ln, L = self._pcm(pcm, lens)
+        n = a.shape[0]
+        nf = max(1, (a.shape[1] - 1) // 480) if a.shape[1] > 480 else 1
+        out = np.empty_like(a)
+        olen = np.empty(n, np.int32)
+        sp = np.zeros((n, nf), np.uint8)
+        self._check(self.lib.mmla_vad_remove_silence(
+            self.h, _ptr(a), n, a.shape[1], _ptr(ln), L, int(items_per_stream), _ptr(out),
+            _ptr(olen), _ptr(sp), nf, 0), 'mmla_vad_remove_silence')
+        lens_in = ln if ln is not None else np.full(n, L, np.int32)
+        nfr = [(int(m) - 1) // 480 if m > 480 else 0 for m in lens_in]
+        return [out[i, :olen[i]].copy() for i in range(n)], [sp[i, :nfr[i]].astype(bool) for i in range(n)]
+
+    def vad_collect(self, pcm, speech, lens=None):
+        """the collector + rewrite alone on given per-frame decisions (list of bool arrays)"""
+        a, ln, L = self._pcm(pcm, lens)
+        n = a.shape[0]
+        nf = max([1] + [len(s) for s in speech])
+        sp = np.zeros((n, nf), np.uint8)
+        for i, s in enumerate(speech):
+            sp[i, :len(s)] = np.asarray(s, np.uint8)
+        out = np.empty_like(a)
+        olen = np.empty(n, np.int32)
+        self._check(self.lib.mmla_vad_collect(self.h, _ptr(a), n, a.shape[1], _ptr(ln), L, _ptr(sp),
+                                              nf, _ptr(out), _ptr(olen), 0), 'mmla_vad_collect')
+        return [out[i, :olen[i]].copy() for i in range(n)]
+
+    def pcm16(self, y):
+        """float audio -> int16 as soundfile writes PCM_16"""
+        a = np.ascontiguousarray(y, dtype=np.float32)
+        out = np.empty(a.shape, np.int16)
+        self._check(self.lib.mmla_pcm16(self.h, _ptr(a), a.size, _ptr(out), 0), 'mmla_pcm16')
+        return out
 
     # -- host-array API -----------------------------------------------------------------------
     @staticmethod

@@ -18,6 +18,7 @@
 #include "od_fe.h"
 #include "si_fe.h"
 #include "nr.h"
+#include "vad.h"
 
 namespace {
 
@@ -125,6 +126,8 @@ struct mmla_ctx {
   int64_t range_reruns = 0;
   bool od_f32_only = false, si_f32_only = false;   // weights outside the fp16 range
   bool loading_f16_bad = false;                     // mmla_load_weights scratch
+  VadState* vad_state = nullptr;   // mmla_vad_reset: webrtcvad.Vad(mode) per stream (device)
+  int64_t vad_streams = 0;
   NrTables* nr_tables = nullptr;   // noise gate (nr.hip): tables + the noise profile's threshold
   float* nr_thresh = nullptr;
   bool nr_ready = false;
@@ -280,7 +283,8 @@ int ws_check_guards(mmla_ctx* c) {
 enum Slot {
   S_PCM = 0, S_LENS, S_IMG, S_X, S_T1, S_T2, S_T3, S_SEQ, S_HOUT, S_LOGIT, S_FEAT, S_SILENT,
   S_OUT0, S_OUT1, S_OUT2, S_OUT3, S_IN, S_FESCR,
-  S_NR_S, S_NR_BITS, S_NR_FMAX, S_NR_FRAMES, S_NR_ITEMS, S_NR_Y, S_NR_ROWS
+  S_NR_S, S_NR_BITS, S_NR_FMAX, S_NR_FRAMES, S_NR_ITEMS, S_NR_Y, S_NR_ROWS,
+  S_VAD_SPEECH, S_VAD_OUT, S_VAD_LENS
 };
 
 // ---- weights -------------------------------------------------------------------------------------
@@ -941,6 +945,7 @@ int mmla_destroy(mmla_ctx* c) {
   if (c->nr_tables) (void)hipFree(c->nr_tables);
   if (c->nr_thresh) (void)hipFree(c->nr_thresh);
   if (c->range_dev) (void)hipFree(c->range_dev);
+  if (c->vad_state) (void)hipFree(c->vad_state);
   if (c->range_host) (void)hipHostFree(c->range_host);
   (void)prof_collect(c);
   for (hipEvent_t e : c->prof_pool) (void)hipEventDestroy(e);
@@ -1469,6 +1474,130 @@ int mmla_si_pipeline(mmla_ctx* c, const int16_t* pcm, int64_t n, int64_t stride,
       return MMLA_OK;
     });
   }));
+  return finish(c, dev);
+}
+
+// ---- silence removal: webrtcvad + vad_collector, soundfile PCM_16 ------------
+
+int mmla_vad_reset(mmla_ctx* c, int64_t n_streams, int32_t mode) {
+  if (!c) return MMLA_E_INVALID;
+  if (n_streams < 1) return fail(c, MMLA_E_INVALID, "n_streams must be >= 1");
+  VadState init;
+  if (!vad_init_state(&init, mode)) return fail(c, MMLA_E_INVALID, "VAD mode must be 0..3, got %d", mode);
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (c->vad_state) HIPCHK(c, hipFree(c->vad_state));
+  c->vad_state = nullptr;
+  c->vad_streams = 0;
+  if (hipMalloc(&c->vad_state, n_streams * sizeof(VadState)) != hipSuccess) {
+    (void)hipGetLastError();
+    return fail(c, MMLA_E_OOM, "VAD state for %lld streams", (long long)n_streams);
+  }
+  std::vector<VadState> h(n_streams, init);
+  HIPCHK(c, hipMemcpy(c->vad_state, h.data(), n_streams * sizeof(VadState), hipMemcpyHostToDevice));
+  c->vad_streams = n_streams;
+  return MMLA_OK;
+}
+
+// shared body: speech == nullptr -> decisions from the context's VAD states, else the caller's
+static int vad_run(mmla_ctx* c, const int16_t* pcm, int64_t n, int64_t stride, const int32_t* lens,
+                   int32_t clip_len, int64_t items_per_stream, const uint8_t* speech_in,
+                   uint8_t* speech_out, int32_t max_frames, int16_t* out, int32_t* out_lens,
+                   uint32_t flags) {
+  if (n < 0 || (n > 0 && (!pcm || !out || !out_lens)) || (!lens && clip_len < 0) ||
+      (n > 1 && stride < (lens ? 1 : clip_len)))
+    return fail(c, MMLA_E_INVALID, "bad VAD args");
+  if (n == 0) return MMLA_OK;
+  const int64_t width = lens ? stride : std::max<int64_t>(clip_len, 1);
+  if (max_frames <= 0) max_frames = std::max(1, vad_frames(width));
+  if (max_frames > 4096) return fail(c, MMLA_E_INVALID, "more than 4096 frames (2 min) per item");
+  HIPCHK(c, hipSetDevice(c->device));
+  const bool dev = flags & MMLA_DEVICE_PTR;
+  VadArgs a{};
+  a.stride = n > 1 ? stride : width;
+  a.clip_len = clip_len;
+  a.n_items = n;
+  a.items_per_stream = items_per_stream;
+  a.max_frames = max_frames;
+  a.state = c->vad_state;
+  const size_t samples = (size_t)(n - 1) * a.stride + width;
+  a.pcm = pcm;
+  a.lens = lens;
+  if (!dev) {
+    void *pp = nullptr, *pl = nullptr;
+    CHK(ws_get(c, S_PCM, samples * sizeof(int16_t), &pp));
+    HIPCHK(c, hipMemcpyAsync(pp, pcm, samples * sizeof(int16_t), hipMemcpyHostToDevice, c->stream));
+    a.pcm = static_cast<int16_t*>(pp);
+    if (lens) {
+      CHK(ws_get(c, S_LENS, n * sizeof(int32_t), &pl));
+      HIPCHK(c, hipMemcpyAsync(pl, lens, n * sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
+      a.lens = static_cast<int32_t*>(pl);
+    }
+  }
+  void* ps = nullptr;
+  const size_t sbytes = (size_t)n * max_frames;
+  if (speech_in && dev) {
+    a.speech = const_cast<uint8_t*>(speech_in);
+  } else if (speech_out && dev) {
+    a.speech = speech_out;
+  } else {
+    CHK(ws_get(c, S_VAD_SPEECH, sbytes, &ps));
+    a.speech = static_cast<uint8_t*>(ps);
+    if (speech_in) HIPCHK(c, hipMemcpyAsync(ps, speech_in, sbytes, hipMemcpyHostToDevice, c->stream));
+  }
+  CHK(out_ptr(c, out, 0, samples, dev, S_VAD_OUT, &a.out));
+  CHK(out_ptr(c, out_lens, 0, n, dev, S_VAD_LENS, &a.out_lens));
+  if (!speech_in) {
+    if (!c->vad_state) return fail(c, MMLA_E_INVALID, "mmla_vad_reset must be called first");
+    if (items_per_stream < 1 || n % items_per_stream || n / items_per_stream != c->vad_streams)
+      return fail(c, MMLA_E_INVALID, "%lld items are not %lld streams x items_per_stream %lld",
+                  (long long)n, (long long)c->vad_streams, (long long)items_per_stream);
+    // the rewrite keeps a frame's bytes or drops it: outputs are never longer than inputs
+    LAUNCH(c, MMLA_STAGE_GLUE, (double)n * width, vad_speech_launch(a, c->stream));
+  }
+  LAUNCH(c, MMLA_STAGE_GLUE, (double)n * width, vad_collect_launch(a, c->stream));
+  CHK(copy_back(c, out, 0, a.out, samples, dev));
+  CHK(copy_back(c, out_lens, 0, a.out_lens, n, dev));
+  if (speech_out && !dev)
+    HIPCHK(c, hipMemcpyAsync(speech_out, a.speech, sbytes, hipMemcpyDeviceToHost, c->stream));
+  return finish(c, dev);
+}
+
+int mmla_vad_remove_silence(mmla_ctx* c, const int16_t* pcm, int64_t n_items, int64_t stride,
+                            const int32_t* lens, int32_t clip_len, int64_t items_per_stream,
+                            int16_t* out, int32_t* out_lens, uint8_t* speech, int32_t max_frames,
+                            uint32_t flags) {
+  if (!c) return MMLA_E_INVALID;
+  return vad_run(c, pcm, n_items, stride, lens, clip_len, items_per_stream, nullptr, speech,
+                 max_frames, out, out_lens, flags);
+}
+
+int mmla_vad_collect(mmla_ctx* c, const int16_t* pcm, int64_t n_items, int64_t stride,
+                     const int32_t* lens, int32_t clip_len, const uint8_t* speech, int32_t max_frames,
+                     int16_t* out, int32_t* out_lens, uint32_t flags) {
+  if (!c) return MMLA_E_INVALID;
+  if (n_items > 0 && !speech) return fail(c, MMLA_E_INVALID, "speech flags required");
+  return vad_run(c, pcm, n_items, stride, lens, clip_len, 1, speech, nullptr, max_frames, out,
+                 out_lens, flags);
+}
+
+int mmla_pcm16(mmla_ctx* c, const float* y, int64_t n, int16_t* out, uint32_t flags) {
+  if (!c) return MMLA_E_INVALID;
+  if (n < 0 || (n > 0 && (!y || !out))) return fail(c, MMLA_E_INVALID, "bad pcm16 args");
+  if (n == 0) return MMLA_OK;
+  HIPCHK(c, hipSetDevice(c->device));
+  const bool dev = flags & MMLA_DEVICE_PTR;
+  const float* dy = y;
+  if (!dev) {
+    void* p = nullptr;
+    CHK(ws_get(c, S_IN, n * sizeof(float), &p));
+    HIPCHK(c, hipMemcpyAsync(p, y, n * sizeof(float), hipMemcpyHostToDevice, c->stream));
+    dy = static_cast<float*>(p);
+  }
+  int16_t* d;
+  CHK(out_ptr(c, out, 0, n, dev, S_VAD_OUT, &d));
+  LAUNCH(c, MMLA_STAGE_GLUE, (double)n * 6, pcm16_launch(dy, n, d, c->stream));
+  CHK(copy_back(c, out, 0, d, n, dev));
   return finish(c, dev);
 }
 

@@ -33,8 +33,16 @@ quantisation edge (tests allow that, see tests/test_oracle_golden.py).
     keeps state in a mutable default argument (:122), so a second call numbers new speakers from 0
     again (si_experiment_golden.npz).
 
-Output: tests/golden/od_golden.npz, si_golden.npz, seg_golden.npz, si_experiment_golden.npz
-(small, compressed).  ``python tests/golden/make_golden.py exp`` regenerates only the last.
+  * the silence removal of save_wave_file(silence_remove=True) (record_on_pc.py:200-295:
+    frame_generator, vad_collector, the rewrite) with a stub is_speech whose per-frame answers are
+    recorded with the output (vad_golden.npz) -- webrtcvad itself is absent (oracle/webrtc_vad.py).
+
+  * the offline SpeakerIdentification flow post_analysing (speaker_identification_post_processing.py:
+    191-312) on one conversation with a stub is_speech and a stub model: silent segments, the
+    window <-> segment mapping, labels and the log text (sipost_golden.npz).
+
+Output: tests/golden/{od,si,seg,si_experiment,vad,sipost}_golden.npz (small, compressed).
+``python tests/golden/make_golden.py exp vad sipost`` regenerates only those parts.
 """
 import hashlib
 import io
@@ -246,7 +254,139 @@ def _experiment_cases(si_mod, tmp):
     return exp
 
 
-def main(parts=('od', 'si', 'seg', 'exp')):
+def _vad_signal(kind):
+    """test signals for the silence-removal rewrite: loud noise blocks ('speech') and quiet ones"""
+    rng = np.random.default_rng(991)
+    if kind == 'gaps':
+        spec = [(0, 4800), (1, 16000), (0, 8000), (1, 8000), (0, 4160)]          # 2.56 s
+    elif kind == 'flicker':
+        spec = [(int(rng.random() < 0.8), 480) for _ in range(85)] + [(0, 160)]
+    elif kind == 'speech':
+        spec = [(1, 40960)]
+    elif kind == 'silent':
+        spec = [(0, 40960)]
+    elif kind == 'retrigger':
+        spec = [(1, 9 * 480), (0, 480), (1, 12 * 480), (0, 11 * 480), (1, 10 * 480), (0, 3 * 480)]
+    elif kind == 'short':
+        spec = [(1, 470)]
+    else:                                                                        # 'exact': 10 frames
+        spec = [(1, 4800)]
+    parts = [(rng.standard_normal(n) * (6000 if loud else 40)).clip(-32768, 32767) for loud, n in spec]
+    return np.concatenate(parts).astype(np.int16)
+
+
+VAD_CASES = ['gaps', 'flicker', 'speech', 'silent', 'retrigger', 'short', 'exact']
+
+
+def _vad_cases(tmp):
+    """record_on_pc.py save_wave_file(silence_remove=True) with a stub is_speech (mean |x| > 300):
+    pins frame_generator + vad_collector + the rewrite (:200-295), not webrtcvad itself"""
+    import scipy.io.wavfile as wavfile
+    for name in ('cv2', 'noisereduce', 'soundfile', 'requests', 'pyaudio',
+                 'skimage', 'skimage.metrics', 'skimage.metrics._structural_similarity'):
+        _module(name, PyAudio=_Anything, paInt16=8, structural_similarity=_Anything)
+    sys.modules.setdefault('overlap_features_generator', _module('overlap_features_generator',
+                                                                 OverlapFeaturesGenerator=_Anything))
+    rec = _load_reference('OverlapDetection/scripts/record_on_pc.py', 'ref_record')
+
+    class StubVad:
+        def __init__(self):
+            self.flags = []
+
+        def is_speech(self, buf, sr):
+            assert sr == 16000 and len(buf) == 960
+            s = bool(np.abs(np.frombuffer(buf, '<i2').astype(np.int64)).mean() > 300)
+            self.flags.append(s)
+            return s
+
+    out = {'names': np.array(VAD_CASES)}
+    for i, kind in enumerate(VAD_CASES):
+        pcm = _vad_signal(kind)
+        stub = StubVad()
+        rec.vad = stub
+        path = os.path.join(tmp, f'vad{i}.wav')
+        rec.save_wave_file(path, [pcm.tobytes()], noise_reduce=False, silence_remove=True)
+        _, y = wavfile.read(path) if os.path.getsize(path) > 44 else (16000, np.zeros(0, np.int16))
+        out[f'pcm_{i}'] = pcm
+        out[f'flags_{i}'] = np.array(stub.flags, bool)
+        out[f'out_{i}'] = np.asarray(y, np.int16)
+        print('VAD', kind, len(pcm), '->', len(y), 'frames', len(stub.flags), 'speech', sum(stub.flags))
+    return out
+
+
+SIPOST_SPEAKERS = ['alice.wav', 'bob.wav', 'carol.wav']
+
+
+def _sipost_case(si_mod, tmp):
+    """post_analysing (speaker_identification_post_processing.py:191-312) on one synthetic
+    conversation with a stub is_speech (mean |x| > 300, answers recorded) and a stub model whose
+    window i scores speaker (i + 1) mod 3 highest: pins the silent-segment logic, the
+    window <-> segment mapping, the labels and the log text (timestamps from a fixed clock)"""
+    import datetime as _dt
+    sys.modules['speaker_identification'] = si_mod
+    _module('speaker_time_distribution')
+    _module('keyboard')
+    _module('pydub', AudioSegment=_Anything, effects=_Anything)
+    for name in ('noisereduce', 'soundfile', 'requests', 'pyaudio'):
+        _module(name, PyAudio=_Anything, paInt16=8)
+    post = _load_reference('SpeakerIdentification/scripts/speaker_identification_post_processing.py',
+                           'ref_si_post')
+    sys.modules['speaker_identification_post_processing'] = post
+    rec = _load_reference('SpeakerIdentification/scripts/record_on_pc.py', 'ref_si_record')
+    sys.modules['record_on_pc'] = rec
+
+    root = os.path.join(tmp, 'sipost')
+    post.Root_Dir = root
+    corpus = os.path.join(root, 'experiment', 'corpus')
+    segdir = os.path.join(root, 'experiment', 'recordings', 'post-time', 'segments', 'conv0')
+    stddir = os.path.join(root, 'experiment', 'recordings', 'post-time', 'standardized')
+    for d in (corpus, segdir, stddir, os.path.join(root, 'experiment', 'logs')):
+        os.makedirs(d, exist_ok=True)
+    for f in SIPOST_SPEAKERS:
+        open(os.path.join(corpus, f), 'wb').close()
+    rng = np.random.default_rng(77)
+    loud = [1, 0, 1, 1, 0]                        # 2.56 s segments: speech / silence
+    whole = np.concatenate([(rng.standard_normal(40960) * (6000 if l else 40)).astype(np.int16)
+                            for l in loud] + [(rng.standard_normal(8000) * 6000).astype(np.int16)])
+    _write_wav(os.path.join(stddir, 'conv0.wav'), whole)
+    for j in range(len(loud)):
+        _write_wav(os.path.join(segdir, f'conv0_{j}_16000_split.wav'), whole[40960 * j:40960 * (j + 1)])
+
+    class StubVad:
+        def __init__(self):
+            self.flags = []
+
+        def is_speech(self, buf, sr):
+            s = bool(np.abs(np.frombuffer(buf, '<i2').astype(np.int64)).mean() > 300)
+            self.flags.append(s)
+            return s
+
+    class StubModel:
+        def predict(self, x):
+            p = np.full((len(x), 3), 0.1)
+            p[np.arange(len(x)), (np.arange(len(x)) + 1) % 3] = 0.8
+            return p
+
+    class FixedClock(_dt.datetime):
+        @classmethod
+        def today(cls):
+            return _dt.datetime(2026, 10, 16, 12, 0, 0)
+
+    stub = StubVad()
+    post.vad = stub
+    post.datetime = FixedClock
+    sys.modules['tensorflow'].keras.models.load_model = lambda path: StubModel()
+    post.post_analysing()
+    log = open(os.path.join(root, 'experiment', 'logs', 'conv0.txt')).read()
+    speakers = sorted(os.listdir(corpus))
+    listing = os.listdir(corpus)
+    print('SIPOST', len(stub.flags), 'frame decisions;', log.count('silent'), 'silent windows')
+    return {'whole': whole, 'flags': np.array(stub.flags, bool), 'log': np.array(log),
+            'corpus_listing': np.array(listing), 'speakers': np.array(speakers),
+            'segment_len': np.array(40960), 'n_segments': np.array(len(loud))}
+
+
+def main(parts=('od', 'si', 'seg', 'exp', 'vad', 'sipost')):
     _install_stubs()
     ofg_mod = _load_reference('OverlapDetection/scripts/overlap_features_generator.py', 'ref_ofg')
     si_mod = _load_reference('SpeakerIdentification/scripts/speaker_identification.py', 'ref_si')
@@ -254,6 +394,10 @@ def main(parts=('od', 'si', 'seg', 'exp')):
     assert ofg.get_attributes() == (400, 160, 16000)
 
     tmp = tempfile.mkdtemp(prefix='mmla_golden_')
+    if 'vad' in parts:
+        np.savez_compressed(os.path.join(HERE, 'vad_golden.npz'), **_vad_cases(tmp))
+    if 'sipost' in parts:
+        np.savez_compressed(os.path.join(HERE, 'sipost_golden.npz'), **_sipost_case(si_mod, tmp))
     if 'exp' in parts:
         np.savez_compressed(os.path.join(HERE, 'si_experiment_golden.npz'),
                             **_experiment_cases(si_mod, tmp))
@@ -302,4 +446,4 @@ def main(parts=('od', 'si', 'seg', 'exp')):
 
 
 if __name__ == '__main__':
-    main(tuple(sys.argv[1:]) or ('od', 'si', 'seg', 'exp'))
+    main(tuple(sys.argv[1:]) or ('od', 'si', 'seg', 'exp', 'vad', 'sipost'))
