@@ -8,9 +8,7 @@
 //   zero_crossing_rate(400, 160)        :100  (edge padding, signbit crossings)
 //   generate_zcr_image + imsave + decode_png   :133-151, record_on_pc.py:156-158
 //
-// Two kernels share the ABI (OdFeArgs); `od_fe_launch` runs v2 unless MMLA_FE_IMPL=1.
-//
-// v2 (default).  One wave = one clip (64-thread workgroups), frames in rounds of R = 6.  The
+// v2.  One wave = one clip (64-thread workgroups), frames in rounds of R = 6.  The
 // 400-point real DFT of a frame is ONE 200-point complex FFT of the even/odd-packed frame
 // z[m] = x[2m] + i x[2m+1] followed by the standard split
 //     X[k] = (Z[k] + conj Z[200-k]) / 2 - i W400^k (Z[k] - conj Z[200-k]) / 2,
@@ -25,9 +23,6 @@
 // window (register prefetch) and the mel-dB scratch stores stay in flight across passes.  The
 // clip's normalisation needs the clip-global max/min, so the dB rows go to a frame-major HBM
 // scratch that the epilogue re-reads (8-band column blocks, transposed through LDS).
-//
-// v1.  The earlier schedule (16 x 25 factoring of the real DFT, 5-frame groups, block barriers);
-// kept for A/B measurements.
 //
 // Arithmetic is float32 (the reference runs the FFT in float64 and stores complex64; the measured
 // deviation on the normalised log-mel is ~1e-5, tolerance 1e-4).  The scalar steps
@@ -572,311 +567,6 @@ __global__ void __launch_bounds__(NT, 2) od_fe_kernel(OdFeArgs a) {
 
 }  // namespace v2
 
-// ================================================================================================
-namespace v1 {
-
-constexpr int F = 5;             // frames per group: 25 F, 45 F, 128 F lane tasks per pass
-constexpr int NG = (NF + F - 1) / F;
-constexpr int WIN = (F - 1) * HOP + N_FFT;   // samples behind one group of frames
-
-struct Smem {                    // 15.9 KB: ~10 clips in flight per CU
-  int16_t win[WIN + 16];         // reflect-padded window of the group, base = 160 f0 - 200
-  cf t[F][9][25];                // pass 1 output, transformed in place by pass 2a
-  float pw[F][216];              // power spectrum (bins 0..200; 201.. stay 0 for the 10-tap mel dot)
-  int zc[NF + 1];                // ZCR counts of the clip
-  float hann[N_FFT];             // tables the lanes index per task (LDS, not L2 latency)
-  float w400[9][25][2];
-  float w25[5][5][2];
-};
-
-// 400-point real DFT per frame, factored n = 25*n1 + n2, k = k1 + 16*k2:
-//   pass 1 (25 tasks/frame): real 16-point DFT over n1 (via a complex 8-point FFT), k1 = 0..8,
-//                            times W400^(n2*k1)
-//   pass 2 (45 tasks/frame): 5-point DFTs over a (n2 = 5a + b), times W25^(b*c)
-//   pass 3 (45 tasks/frame): 5-point DFTs over b -> X[k1 + 16*(c + 5d)] -> |X|^2; bins > 200
-//                            fold onto 400 - k (conjugate symmetry) for k1 = 1..7
-__global__ void __launch_bounds__(NT) od_fe_kernel(OdFeArgs a) {
-  __shared__ __attribute__((aligned(16))) Smem sm;
-  const OdFeTables& tb = *a.tables;
-  const int lane = threadIdx.x;
-  const int64_t clip = blockIdx.x;
-
-  int len = a.lens ? a.lens[clip] : a.clip_len;
-  len = len < 0 ? 0 : (len > CLIP ? CLIP : len);
-  const int16_t* src = a.pcm + clip * a.clip_stride;
-  float* scr = a.scratch + clip * (NMEL * NF);
-  const int sg_first = (len > 0 ? src[0] : (int16_t)0) < 0;
-  const int sg_last = (CLIP - 1 < len ? src[CLIP - 1] : (int16_t)0) < 0;
-
-  constexpr int WCH = WIN / 8;
-  constexpr int WPL = (WCH + NT - 1) / NT;
-  const bool vec_ok = ((reinterpret_cast<uintptr_t>(src) & 15) == 0);
-  auto fast = [&](int g_) {
-    const int b_ = HOP * g_ * F - N_FFT / 2;
-    return vec_ok && b_ >= 0 && b_ + WIN <= len;
-  };
-  uint4 nxt[WPL];
-  auto prefetch = [&](int g_) {
-    const uint4* s4 = reinterpret_cast<const uint4*>(src + HOP * g_ * F - N_FFT / 2);
-#pragma unroll
-    for (int j = 0; j < WPL; ++j) {
-      const int ch = lane + NT * j;
-      if (ch < WCH) nxt[j] = s4[ch];
-    }
-  };
-  if (fast(0)) prefetch(0);
-
-  for (int i = lane; i < N_FFT; i += NT) sm.hann[i] = tb.hann[i];
-  for (int i = lane; i < 9 * 25 * 2; i += NT) (&sm.w400[0][0][0])[i] = (&tb.w400[0][0][0])[i];
-  for (int i = lane; i < 5 * 5 * 2; i += NT) (&sm.w25[0][0][0])[i] = (&tb.w25[0][0][0])[i];
-  for (int i = lane; i < F * 216; i += NT) (&sm.pw[0][0])[i] = 0.0f;
-  int mst[NMEL / NT];
-  float mw[NMEL / NT][10];
-#pragma unroll
-  for (int mh = 0; mh < NMEL / NT; ++mh) {
-    const int m = lane + NT * mh;
-    mst[mh] = tb.mel_start[m];
-#pragma unroll
-    for (int j = 0; j < 10; ++j) mw[mh][j] = tb.mel_w[m][j];
-  }
-
-  FE_T_INIT
-  float smax = 0.0f, smin = INFINITY;
-  for (int g = 0; g < NG; ++g) {
-    const int f0 = g * F;
-    const int base = HOP * f0 - N_FFT / 2;
-    __syncthreads();
-    if (fast(g)) {
-#pragma unroll
-      for (int j = 0; j < WPL; ++j) {
-        const int ch = lane + NT * j;
-        if (ch < WCH) reinterpret_cast<uint4*>(sm.win)[ch] = nxt[j];
-      }
-    } else {
-      for (int w = lane; w < WIN; w += NT) {
-        int i = base + w;
-        i = i < 0 ? -i : i;
-        i = i >= CLIP ? 2 * (CLIP - 1) - i : i;
-        sm.win[w] = i < len ? src[i] : (int16_t)0;
-      }
-    }
-    if (g + 1 < NG && fast(g + 1)) prefetch(g + 1);
-    __syncthreads();
-    FE_MARK(0);
-    {
-      constexpr int ZCH = 20, ZL = WIN / ZCH;
-      static_assert(WIN % ZCH == 0 && HOP % ZCH == 0 && N_FFT % ZCH == 0, "ZCR chunking");
-      const bool interior = base >= 0 && base + WIN <= CLIP;
-      auto sgn = [&](int w) {
-        const int i = base + w;
-        return i < 0 ? sg_first : (i >= CLIP ? sg_last : (int)(sm.win[w] < 0));
-      };
-      int cl = 0, first = 0;
-      if (lane < ZL) {
-        const int w0 = ZCH * lane;
-        int prev = w0 == 0 ? -1 : (interior ? (int)(sm.win[w0 - 1] < 0) : sgn(w0 - 1));
-#pragma unroll
-        for (int j = 0; j < ZCH; ++j) {
-          const int cur = interior ? (int)(sm.win[w0 + j] < 0) : sgn(w0 + j);
-          const int x = (prev >= 0) & (cur != prev);
-          cl += x;
-          if (j == 0) first = x;
-          prev = cur;
-        }
-      }
-      int* scan = reinterpret_cast<int*>(sm.t);
-      scan[lane] = cl;
-      scan[NT + lane] = first;
-      __syncthreads();
-      if (lane < F && f0 + lane < NF) {
-        int c = 0;
-#pragma unroll
-        for (int l = 0; l < 20; ++l) c += scan[8 * lane + l];
-        sm.zc[f0 + lane] = c - scan[NT + 8 * lane];
-      }
-      __syncthreads();
-    }
-    FE_MARK(1);
-#pragma unroll
-    for (int r = 0; r < (F * 25 + NT - 1) / NT; ++r) {
-      const int task = lane + NT * r;
-      if (task >= F * 25) break;
-      const int f = task / 25, n2 = task - f * 25;
-      const int16_t* x = sm.win + HOP * f;
-      cf z[8];
-#pragma unroll
-      for (int m = 0; m < 8; ++m) {
-        const int ne = 25 * (2 * m) + n2, no = 25 * (2 * m + 1) + n2;
-        z[m] = {(float)x[ne] * (1.0f / 32768.0f) * sm.hann[ne],
-                (float)x[no] * (1.0f / 32768.0f) * sm.hann[no]};
-      }
-      fft8(z);
-#pragma unroll
-      for (int k = 0; k <= 8; ++k) {
-        cf zk = z[k & 7], zr = cconj(z[(8 - k) & 7]);
-        cf e = cscale(cadd(zk, zr), 0.5f);
-        cf d = csub(zk, zr);
-        cf o = {0.5f * d.y, -0.5f * d.x};
-        cf w16 = {tb.w16[k][0], tb.w16[k][1]};
-        cf y = cadd(e, cmul(w16, o));
-        cf tw = {sm.w400[k][n2][0], sm.w400[k][n2][1]};
-        sm.t[f][k][n2] = cmul(y, tw);
-      }
-    }
-    __syncthreads();
-    FE_MARK(2);
-#pragma unroll
-    for (int rr = 0; rr < (F * 45 + NT - 1) / NT; ++rr) {
-      const int task = lane + NT * rr;
-      if (task >= F * 45) break;
-      const int f = task / 45, r = task - f * 45, k1 = r / 5, b = r - k1 * 5;
-      cf y[5];
-      dft5(sm.t[f][k1][b], sm.t[f][k1][5 + b], sm.t[f][k1][10 + b], sm.t[f][k1][15 + b],
-           sm.t[f][k1][20 + b], y);
-#pragma unroll
-      for (int c = 0; c < 5; ++c) {
-        cf tw = {sm.w25[b][c][0], sm.w25[b][c][1]};
-        sm.t[f][k1][c * 5 + b] = cmul(y[c], tw);
-      }
-    }
-    __syncthreads();
-    FE_MARK(3);
-#pragma unroll
-    for (int rr = 0; rr < (F * 45 + NT - 1) / NT; ++rr) {
-      const int task = lane + NT * rr;
-      if (task >= F * 45) break;
-      const int f = task / 45, r = task - f * 45, k1 = r / 5, c = r - k1 * 5;
-      cf y[5];
-      dft5(sm.t[f][k1][c * 5 + 0], sm.t[f][k1][c * 5 + 1], sm.t[f][k1][c * 5 + 2],
-           sm.t[f][k1][c * 5 + 3], sm.t[f][k1][c * 5 + 4], y);
-#pragma unroll
-      for (int d = 0; d < 5; ++d) {
-        const int bin = k1 + 16 * (c + 5 * d);
-        const float p = fmaf(y[d].x, y[d].x, y[d].y * y[d].y);
-        if (bin <= 200)
-          sm.pw[f][bin] = p;
-        else if (k1 >= 1 && k1 <= 7)
-          sm.pw[f][N_FFT - bin] = p;
-      }
-    }
-    __syncthreads();
-    FE_MARK(4);
-#pragma unroll
-    for (int mh = 0; mh < NMEL / NT; ++mh) {
-      const int m = lane + NT * mh;
-#pragma unroll
-      for (int f = 0; f < F; ++f) {
-        if (f0 + f >= NF) break;
-        const float* p = &sm.pw[f][mst[mh]];
-        float acc = 0.0f;   // the band's non-zeros in order, then exact zero terms: same result
-#pragma unroll
-        for (int j = 0; j < 10; ++j) acc = fmaf(mw[mh][j], p[j], acc);
-        scr[(f0 + f) * NMEL + m] = 10.0f * log10f(fmaxf(1e-10f, acc));
-        smax = fmaxf(smax, acc);
-        smin = fminf(smin, acc);
-      }
-    }
-  }
-  FE_MARK(5);
-  smax = wave_max(smax);
-  smin = wave_min(smin);
-  __threadfence();
-  __syncthreads();
-  {
-#pragma clang fp contract(off)
-  const float amin = 1e-10f;
-  const float ref_db = (float)(10.0 * log10(fmax(1e-10, (double)smax)));
-  const float d_max = 10.0f * log10f(fmaxf(amin, smax)) - ref_db;
-  const float thr = d_max - 80.0f;
-  const float d_min = fmaxf(10.0f * log10f(fmaxf(amin, smin)) - ref_db, thr);
-  const float diff = d_max - d_min;
-
-  float* db_out = a.db ? a.db + clip * (NMEL * NF) : nullptr;
-  float* nm_out = a.norm ? a.norm + clip * (NMEL * NF) : nullptr;
-  if (a.zcr) {
-    for (int f = lane; f < NF; f += NT) a.zcr[clip * NF + f] = (float)sm.zc[f] * (1.0f / 400.0f);
-  }
-  constexpr int MB = 8;
-  float* nvt = reinterpret_cast<float*>(&sm.t[0][0][0]);
-  float* dbt = nvt + NF * MB;
-  uint8_t* rb = reinterpret_cast<uint8_t*>(sm.win);
-  static_assert(sizeof(sm.t) + sizeof(sm.pw) >= 2 * NF * MB * sizeof(float), "LDS tiles");
-  for (int w = lane; w < NF; w += NT) rb[w] = (uint8_t)(int)(((double)sm.zc[w] / 400.0) * 255.0);
-  const float inv_diff = 1.0f / diff;
-  constexpr int RPL = (NF * MB / 4 + NT - 1) / NT;
-  float4 cur[RPL], nxt2[RPL];
-  auto fetch = [&](int mb_, float4 (&dst)[RPL]) {
-#pragma unroll
-    for (int r = 0; r < RPL; ++r) {
-      const int i = lane + NT * r;
-      const int t = i / (MB / 4), qd = i - t * (MB / 4);
-      if (i < NF * MB / 4) dst[r] = *reinterpret_cast<const float4*>(scr + t * NMEL + MB * mb_ + 4 * qd);
-    }
-  };
-  fetch(0, nxt2);
-  for (int mb = 0; mb < NMEL / MB; ++mb) {
-#pragma unroll
-    for (int r = 0; r < RPL; ++r) cur[r] = nxt2[r];
-    if (mb + 1 < NMEL / MB) fetch(mb + 1, nxt2);
-    __syncthreads();
-#pragma unroll
-    for (int r = 0; r < RPL; ++r) {
-      const int i = lane + NT * r;
-      if (i >= NF * MB / 4) break;
-      const int t = i / (MB / 4), qd = i - t * (MB / 4);
-      const float pv[4] = {cur[r].x, cur[r].y, cur[r].z, cur[r].w};
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        float d = pv[j] - ref_db;
-        d = fmaxf(d, thr);
-        dbt[t * MB + 4 * qd + j] = d;
-        nvt[t * MB + 4 * qd + j] = (d - d_min) * inv_diff;
-      }
-    }
-    __syncthreads();
-    if (db_out || nm_out) {
-      for (int e = lane; e < MB * NF; e += NT) {
-        const int r = e / NF, t = e - r * NF;
-        const int o = (MB * mb + r) * NF + t;
-        if (db_out) db_out[o] = dbt[t * MB + r];
-        if (nm_out) nm_out[o] = nvt[t * MB + r];
-      }
-    }
-    if (a.img) {
-      const int h_lo = NMEL - MB * (mb + 1);
-      uint32_t* out = reinterpret_cast<uint32_t*>(a.img + clip * (NMEL * NF * 3) + h_lo * NF * 3);
-      for (int qd = lane; qd < MB * NF / 4; qd += NT) {
-        uint32_t by[12];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int p = 4 * qd + j;
-          const int hr = p / NF, w = p - hr * NF;
-          const double v = (1.0 - (double)nvt[w * MB + (MB - 1 - hr)]) * 255.0;
-          const uint32_t gb = (v >= 0.0) ? ((uint32_t)(int)v & 255u) : 0u;
-          by[3 * j] = rb[w];
-          by[3 * j + 1] = gb;
-          by[3 * j + 2] = gb;
-        }
-#pragma unroll
-        for (int k = 0; k < 3; ++k)
-          out[3 * qd + k] = by[4 * k] | (by[4 * k + 1] << 8) | (by[4 * k + 2] << 16) | (by[4 * k + 3] << 24);
-      }
-    }
-  }
-  }
-  FE_MARK(6);
-  FE_T_STORE
-}
-
-}  // namespace v1
-
-int fe_impl() {
-  static const int impl = [] {
-    const char* e = getenv("MMLA_FE_IMPL");
-    return (e && atoi(e) == 1) ? 1 : 2;
-  }();
-  return impl;
-}
 
 }  // namespace
 
@@ -886,7 +576,7 @@ extern "C" int mmla_debug_fe_times(unsigned long long* host) {
 }
 #endif
 
-size_t od_fe_smem_bytes() { return fe_impl() == 1 ? sizeof(v1::Smem) : sizeof(v2::Smem); }
+size_t od_fe_smem_bytes() { return sizeof(v2::Smem); }
 
 bool od_fe_tables_ok(const OdFeTables& t) {
   if (t.mel_taps_lo > v2::T_LO || t.mel_taps_hi > v2::T_HI) return false;
@@ -913,10 +603,7 @@ static void launch_v2(const OdFeArgs& a, int64_t n, hipStream_t s) {
 hipError_t od_fe_launch(const OdFeArgs& a, int64_t n_clips, hipStream_t stream) {
   if (n_clips <= 0) return hipSuccess;
   if (!a.scratch) return hipErrorInvalidValue;
-  if (fe_impl() == 1)
-    hipLaunchKernelGGL(v1::od_fe_kernel, dim3((unsigned)n_clips), dim3(NT), 0, stream, a);
-  else
-    launch_v2(a, n_clips, stream);
+  launch_v2(a, n_clips, stream);
   return hipGetLastError();
 }
 

@@ -11,11 +11,11 @@
 // psf computes in float64; so does this kernel (gfx950 fp64 VALU), so parity is ~1e-12, not the
 // ~4e-5 an fp32 FFT gives (SURVEY.md 7 "Hard parts").  Output is stored float32 (predict casts).
 //
-// Both kernels compute a 512-point real FFT per frame as a 256-point complex FFT of the packed frame
+// The kernel computes a 512-point real FFT per frame as a 256-point complex FFT of the packed frame
 // (s[2n] + i s[2n+1]) factored 16 x 16, then the real split; only min(T, 260) frames are computed
-// (delta-delta of row 255 reaches feat[259]).  `si_fe_launch` runs v2 unless MMLA_SI_FE_IMPL=1.
+// (delta-delta of row 255 reaches feat[259]).
 //
-// v2 (default).  One wave = one clip (64-thread workgroups, ~19.7 KB LDS: 8 clips in flight per
+// v2.  One wave = one clip (64-thread workgroups, ~19.7 KB LDS: 8 clips in flight per
 // CU), frames in rounds of R = 4, no block barriers (a wave's LDS operations execute in issue
 // order).  Per round:
 //   window   the round's 888 samples, register-prefetched one round ahead (16-B chunks)
@@ -33,8 +33,6 @@
 //   dct      lane (f, c): 26-term dot with the lifted DCT row held in registers; c0 = log energy
 // Cepstra go straight to the output rows (halo frames to LDS); the epilogue re-reads them into LDS
 // and writes the deltas (the clip's 264 x 13 cepstra do not fit beside the round buffers).
-//
-// v1.  One workgroup (256 threads) per clip, 12-frame tiles, block barriers; kept for A/B runs.
 #include "common.h"
 #include "si_fe.h"
 
@@ -58,218 +56,6 @@ MMLA_DEV void fft4c(C& a0, C& a1, C& a2, C& a3) {
 }
 
 // ================================================================================================
-namespace v1 {
-
-constexpr int NT = 256;
-constexpr int FT = 12;          // frames per tile: LDS 64 KB -> 2 workgroups per CU
-
-struct Smem {
-  cd buf[FT][256];      // pass A output -> (in place) Z -> (in place) power spectrum [f][258]
-  double lfe[FT][28];   // log filterbank energies + log energy
-  float feat[NL][13];   // cepstra (float64 math, stored float32: the deltas' inputs); the deltas
-                        // themselves are recomputed per output element instead of staged
-};
-
-// complex 16-point DFT in registers, radix 4 x 4: in v[n], out v[4*q1 + q2] = Y[q1 + 4*q2]
-MMLA_DEV void dft16(cd v[16], const double (*w16)[2]) {
-#pragma unroll
-  for (int m2 = 0; m2 < 4; ++m2) fft4c(v[m2], v[4 + m2], v[8 + m2], v[12 + m2]);
-#pragma unroll
-  for (int q1 = 1; q1 < 4; ++q1)
-#pragma unroll
-    for (int m2 = 1; m2 < 4; ++m2) {
-      const int e = m2 * q1;   // W16^(m2 q1)
-      const cd w = {w16[e][0], w16[e][1]};
-      v[4 * q1 + m2] = cmul(v[4 * q1 + m2], w);
-    }
-#pragma unroll
-  for (int q1 = 0; q1 < 4; ++q1) fft4c(v[4 * q1 + 0], v[4 * q1 + 1], v[4 * q1 + 2], v[4 * q1 + 3]);
-}
-
-// pre-emphasised sample s[i] = x[i] - 0.97 x[i-1] (s[0] = x[0]); 0 beyond the signal
-MMLA_DEV double pre(const int16_t* x, int64_t i, int64_t len) {
-#pragma clang fp contract(off)
-  if (i >= len) return 0.0;
-  return i == 0 ? (double)x[0] : (double)x[i] - 0.97 * (double)x[i - 1];
-}
-
-__global__ void __launch_bounds__(NT, 2) si_fe_kernel(SiFeArgs a) {
-#pragma clang fp contract(off)   // match numpy's separately rounded float64 ops (preemphasis, etc.)
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-  Smem& sm = *reinterpret_cast<Smem*>(smem_raw);
-  const SiFeTables& tb = *a.tables;
-  const int tid = threadIdx.x;
-  const int64_t blk = blockIdx.x;
-  float* out = a.feat + blk * (OUTF * 39);
-
-  const int16_t* x;
-  int64_t len, frame0;
-  if (a.seq_len > 0) {            // window blk of one long signal (conversation mode)
-    x = a.pcm;
-    len = a.seq_len;
-    frame0 = OUTF * blk;
-  } else {                        // one clip per block (input_feature_gen)
-    x = a.pcm + blk * a.clip_stride;
-    len = a.lens ? a.lens[blk] : a.clip_len;
-    frame0 = 0;
-    if (len < 4000) {             // speaker_identification.py:375-376
-      for (int e = tid; e < OUTF * 39; e += NT) out[e] = 0.0f;
-      if (a.silent && tid == 0) a.silent[blk] = 1;
-      return;
-    }
-    if (a.silent && tid == 0) a.silent[blk] = 0;
-  }
-  const int64_t T = len <= 400 ? 1 : 1 + (len - 400 + 159) / 160;   // framesig numframes
-  // local frame lf <-> global frame g = frame0 - HALO + lf, computed where 0 <= g < T
-  const int64_t g_lo = frame0 - HALO < 0 ? 0 : frame0 - HALO;
-  const int64_t g_hi = frame0 - HALO + NL < T ? frame0 - HALO + NL : T;
-  const int nloc = (int)(g_hi - g_lo);
-  const int lf0 = (int)(g_lo - (frame0 - HALO));
-  double* pw = reinterpret_cast<double*>(&sm.buf[0][0]);
-
-  for (int t0 = 0; t0 < nloc; t0 += FT) {
-    const int nfr = min(FT, nloc - t0);
-    // pass A: task (f, n2): DFT-16 over n1 of z[16 n1 + n2], z[n] = s[2n] + i s[2n+1]
-    for (int task = tid; task < nfr * 16; task += NT) {
-      const int f = task >> 4, n2 = task & 15;
-      const int64_t fs = 160 * (g_lo + t0 + f);
-      cd v[16];
-#pragma unroll
-      for (int n1 = 0; n1 < 16; ++n1) {
-        const int n = 16 * n1 + n2;
-        const bool in = 2 * n < 400;   // rectangular 400-sample frame, zero-padded to 512
-        v[n1] = {in ? pre(x, fs + 2 * n, len) : 0.0, in ? pre(x, fs + 2 * n + 1, len) : 0.0};
-      }
-      dft16(v, tb.w16);
-#pragma unroll
-      for (int q1 = 0; q1 < 4; ++q1)
-#pragma unroll
-        for (int q2 = 0; q2 < 4; ++q2) {
-          const int k1 = q1 + 4 * q2;
-          const cd w = {tb.w256[n2][k1][0], tb.w256[n2][k1][1]};
-          sm.buf[f][k1 * 16 + n2] = cmul(v[4 * q1 + q2], w);
-        }
-    }
-    __syncthreads();
-    // pass B (in place): task (f, k1): DFT-16 over n2 -> Z[k1 + 16 k2]
-    {
-      cd v[16];
-      const int task = tid;
-      const bool act = task < nfr * 16;
-      const int f = task >> 4, k1 = task & 15;
-      if (act) {
-#pragma unroll
-        for (int n2 = 0; n2 < 16; ++n2) v[n2] = sm.buf[f][k1 * 16 + n2];
-        dft16(v, tb.w16);
-      }
-      __syncthreads();
-      if (act) {
-#pragma unroll
-        for (int q1 = 0; q1 < 4; ++q1)
-#pragma unroll
-          for (int q2 = 0; q2 < 4; ++q2) sm.buf[f][k1 + 16 * (q1 + 4 * q2)] = v[4 * q1 + q2];
-      }
-    }
-    __syncthreads();
-    // pass C (in place): real split -> P[f][k] = |X[k]|^2 / 512, k = 0..256, at pw[f*258 + k]
-    {
-      constexpr int PER = (FT * 257 + NT - 1) / NT;
-      double pv[PER];
-#pragma unroll
-      for (int r = 0; r < PER; ++r) {
-        const int task = tid + NT * r;
-        pv[r] = 0.0;
-        if (task < nfr * 257) {
-          const int f = task / 257, k = task - f * 257;
-          const cd zk = sm.buf[f][k & 255];
-          const cd zr = cconj(sm.buf[f][(256 - k) & 255]);
-          const cd e = cscale(cadd(zk, zr), 0.5);
-          const cd d = csub(zk, zr);
-          const cd o = {0.5 * d.y, -0.5 * d.x};
-          const cd w = {tb.w512[k][0], tb.w512[k][1]};
-          const cd X = cadd(e, cmul(w, o));
-          // numpy: square(absolute(X)) / 512 with absolute = hypot; x^2 + y^2 differs from
-          // hypot^2 by an ulp (no fp64 sqrt/div on the hot path)
-          const double mag2 = X.x * X.x + X.y * X.y;
-          pv[r] = mag2 * (1.0 / 512.0);
-        }
-      }
-      __syncthreads();
-#pragma unroll
-      for (int r = 0; r < PER; ++r) {
-        const int task = tid + NT * r;
-        if (task < nfr * 257) {
-          const int f = task / 257, k = task - f * 257;
-          pw[f * 258 + k] = pv[r];
-        }
-      }
-    }
-    __syncthreads();
-    // pass D: 26 filterbank energies + frame energy -> log (0 -> eps)
-    for (int task = tid; task < nfr * 27; task += NT) {
-      const int f = task / 27, j = task - f * 27;
-      const double* p = pw + f * 258;
-      double acc = 0.0;
-      if (j < 26) {
-        const int lo = tb.fb_lo[j], n = tb.fb_hi[j] - lo;
-        for (int i = 0; i < n; ++i) acc += tb.fb_w[j][i] * p[lo + i];
-      } else {
-        for (int i = 0; i < 257; ++i) acc += p[i];
-      }
-      if (acc == 0.0) acc = 2.220446049250313e-16;   // numpy.finfo(float).eps
-      sm.lfe[f][j] = log(acc);
-    }
-    __syncthreads();
-    // pass E: DCT-II ortho x lifter for c = 1..12; c0 = log(energy)
-    for (int task = tid; task < nfr * 13; task += NT) {
-      const int f = task / 13, c = task - f * 13;
-      double v;
-      if (c == 0) {
-        v = sm.lfe[f][26];
-      } else {
-        v = 0.0;
-        for (int j = 0; j < 26; ++j) v += sm.lfe[f][j] * tb.dct[c][j];
-      }
-      sm.feat[lf0 + t0 + f][c] = (float)v;
-    }
-    __syncthreads();
-  }
-
-  // delta(feat, 2): d[g] = (-2 f[g-2] - f[g-1] + f[g+1] + 2 f[g+2]) / 10, edges clamped to the
-  // TRUE sequence [0, T-1] (speaker_identification.py:147 np.pad mode='edge').
-  auto loc = [&](int64_t g) {
-    g = g < 0 ? 0 : (g > T - 1 ? T - 1 : g);
-    return (int)(g - (frame0 - HALO));
-  };
-  // delta of feat column c at global frame g (g clamped by the caller)
-  auto dfe = [&](int64_t g, int c) {
-    const double v = -2.0 * (double)sm.feat[loc(g - 2)][c] - 1.0 * (double)sm.feat[loc(g - 1)][c] +
-                     1.0 * (double)sm.feat[loc(g + 1)][c] + 2.0 * (double)sm.feat[loc(g + 2)][c];
-    return v / 10.0;
-  };
-  auto clampg = [&](int64_t g) { return g < 0 ? (int64_t)0 : (g > T - 1 ? T - 1 : g); };
-  for (int e = tid; e < OUTF * 39; e += NT) {
-    const int t = e / 39, c = e - t * 39;
-    const int64_t g = frame0 + t;
-    float v = 0.0f;
-    if (g < T) {
-      if (c < 13) {
-        v = sm.feat[loc(g)][c];
-      } else if (c < 26) {
-        v = (float)dfe(g, c - 13);
-      } else {
-        // delta of the delta sequence, itself edge-padded at the true ends
-        const int cc = c - 26;
-        const double d = -2.0 * dfe(clampg(g - 2), cc) - 1.0 * dfe(clampg(g - 1), cc) +
-                         1.0 * dfe(clampg(g + 1), cc) + 2.0 * dfe(clampg(g + 2), cc);
-        v = (float)(d / 10.0);
-      }
-    }
-    out[e] = v;
-  }
-}
-
-}  // namespace v1
 
 // ================================================================================================
 namespace v2 {
@@ -645,31 +431,11 @@ __global__ void __launch_bounds__(NT, 2) si_fe_kernel(SiFeArgs a) {
 
 }  // namespace v2
 
-int si_fe_impl() {
-  static const int impl = [] {
-    const char* e = getenv("MMLA_SI_FE_IMPL");
-    return (e && atoi(e) == 1) ? 1 : 2;
-  }();
-  return impl;
-}
-
 }  // namespace
 
 hipError_t si_fe_launch(const SiFeArgs& a, int64_t n_clips, hipStream_t stream) {
   if (n_clips <= 0) return hipSuccess;
-  if (si_fe_impl() == 2) {
-    hipLaunchKernelGGL(v2::si_fe_kernel, dim3((unsigned)n_clips), dim3(v2::NT), 0, stream, a);
-    return hipGetLastError();
-  }
-  const size_t smem = sizeof(v1::Smem);
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(v1::si_fe_kernel),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-    if (e != hipSuccess) return e;
-    attr_set = true;
-  }
-  hipLaunchKernelGGL(v1::si_fe_kernel, dim3((unsigned)n_clips), dim3(v1::NT), smem, stream, a);
+  hipLaunchKernelGGL(v2::si_fe_kernel, dim3((unsigned)n_clips), dim3(v2::NT), 0, stream, a);
   return hipGetLastError();
 }
 

@@ -1,6 +1,6 @@
 """Per-dispatch HBM bytes of the roofline kernels from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes
 (dev tool).  FETCH_SIZE is doubled (gfx950: MI355X_MICROARCH.md, HBM section); both counters are KiB.
-usage: python tools/pmc_traffic.py <workload> <fetch_dir> <write_dir>"""
+usage: python tools/pmc_traffic.py <workload> <fetch_dir> <write_dir> <bench log of the FETCH pass>"""
 import csv
 import glob
 import json
@@ -26,6 +26,14 @@ def read(d, ctr):
     return out
 
 
+def clips_per_launch(bench_log, wl):
+    if bench_log and os.path.exists(bench_log):
+        for line in open(bench_log):
+            if line.startswith('{'):
+                return int(json.loads(line)['config']['microbatch'])
+    raise SystemExit(f'{wl}: need the bench log (its JSON line names the micro-batch)')
+
+
 def main():
     wl, fdir, wdir = sys.argv[1:4]
     fe, wr = read(fdir, 'FETCH_SIZE'), read(wdir, 'WRITE_SIZE')
@@ -48,9 +56,9 @@ def main():
               'read_bytes_per_launch': v['read_bytes'] / max(v['dispatches'], 1),
               'write_bytes_per_launch': v['write_bytes'] / max(v['dispatches'], 1)}
           for s, v in stages.items()}
-    # clips each launch processed: the library's micro-batch (OD 4096, SI 16384) / the od_features
-    # bench batch (4096)
-    cpl = {s: (16384 if wl == 'si_pipeline' else 4096) for s in st}
+    # clips each launch processed: the micro-batch the bench line reports (config.microbatch; the
+    # od_features workload launches its whole batch at once)
+    cpl = {s: clips_per_launch(sys.argv[4] if len(sys.argv) > 4 else None, wl) for s in st}
     json.dump({'workload': wl, 'clips_per_launch': cpl, 'note': 'rocprofv3 --pmc FETCH_SIZE (x2, gfx950) and WRITE_SIZE in '
                'separate passes over `bench.py --workload %s --steps 1 --warmup 0`' % wl,
                'stages': st, 'kernels': kernels}, sys.stdout, indent=1)
