@@ -168,13 +168,17 @@ __global__ void __launch_bounds__(NT) nr_stft_kernel(NrArgs a) {
   uint8_t* bits = a.bits + (item * a.T + t) * NB;
   double mx = -INFINITY;
   if (!load_frame(a, it, t, buf, lane)) {
-    // a window of zeros: S = 0 is never read (nr_gate_kernel only reads frames that reach the
-    // kept interior, which overlap the signal); its mask bits are read by the smoothing rows of
-    // frames within NG_T / 2 of those
+    // a window of zeros: its mask bits are read by the smoothing rows of frames within NG_T / 2
+    // of the kept interior; S = 0 is read by nr_gate_kernel when the frame itself reaches the
+    // interior (a run of >= 1024 zero samples inside the signal), so it is written then -- the
+    // scratch holds the previous call's spectra
     const double dz = db_of_power(0.0);
     const int64_t f_lo = (int64_t)HOP * (t - NG_T / 2) - NFFT / 2, f_hi = (int64_t)HOP * (t + NG_T / 2) + NFFT / 2;
     if (f_lo < a.keep0 + a.keep_len && f_hi > a.keep0)
       for (int k = lane; k < NB; k += NT) bits[k] = dz > (double)a.thresh[k];
+    const int64_t g_lo = (int64_t)HOP * t - NFFT / 2, g_hi = (int64_t)HOP * t + NFFT / 2;
+    if (g_lo < a.keep0 + a.keep_len && g_hi > a.keep0)
+      for (int k = lane; k < NB; k += NT) S[k] = double2{0.0, 0.0};
     mx = dz;
   } else {
     // the split's per-bin tables (bins k = lane + 64 i), loaded under the FFT

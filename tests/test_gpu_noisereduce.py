@@ -91,3 +91,19 @@ def test_silent_signal():
     got = nr.reduce_noise(y=y, sr=16000, y_noise=noise, stationary=True)
     want = onr.reduce_noise(y, 16000, noise)
     assert np.array_equal(got, want.astype(np.float32))
+
+
+def test_zero_run_inside_signal_after_other_calls():
+    """A run of >= 1024 zero samples inside a voiced signal: its all-zero windows still reach the
+    kept interior, so their spectra (0) are read by the gate; the scratch holding the previous
+    call's spectra must not leak in (regression: the first call on a fresh context passed)."""
+    from mmla_audio_amd import _lib
+    noise, ys = _signals()
+    ctx = _lib.Context(0)
+    ctx.nr_set_noise(noise)
+    ctx.nr_reduce(np.stack([ys[0], ys[1]]))                # fill the scratch with nonzero spectra
+    y = ys[1].copy()
+    y[9000:13800] = 0.0
+    y[30000:31100] = 0.0
+    got = ctx.nr_reduce(y)
+    _close(got, onr.reduce_noise(y, 16000, noise))
