@@ -75,7 +75,8 @@ int mmla_synchronize(mmla_ctx* ctx);
  * Arithmetic of the spatial convolutions (98 % of OD-NET FLOPs) and the BiLSTM:
  *   MMLA_PREC_F16X3 (default) error-compensated 3xFP16 on f16 MFMA: operands split hi + 2^-11 lo,
  *                   hi*hi + hi*lo + lo*hi accumulated in f32 (~22-bit products, f32 accumulation);
- *                   needs |activations|, |weights| < 65504 (LSTM: |x| < 1023, |w| < 255.9).
+ *                   needs |activations| < 65504 in the fused res_blocks, < 4094 in the halo-tiled
+ *                   convs (split x 2^4) and < 1023 in the LSTM (x 2^6); |weights| < 255.9 (x 2^8).
  *                   Range guard: weights outside it make that model run exact f32 (decided at
  *                   mmla_load_weights); every kernel that splits an activation flags a value
  *                   outside it.  Host-pointer calls then re-run the micro-batch in exact f32

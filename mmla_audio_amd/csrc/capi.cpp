@@ -319,8 +319,9 @@ int take_conv(mmla_ctx* c, Cursor& cur, std::vector<void*>& al, int kh, int kw, 
   const float* k = cur.take((int64_t)kh * kw * cin * cout);
   const float* b = cur.take(cout);
   if (!cur.ok) return fail(c, MMLA_E_SHAPE, "weight blob too short");
+  // 3xFP16 needs fp16-range weights: conv_h3 splits w * 2^8 (conv_h3.hip), so |w| < 65504 / 2^8
   for (int64_t i = 0; i < (int64_t)kh * kw * cin * cout; ++i)
-    if (!(std::fabs(k[i]) < 65504.0f)) c->loading_f16_bad = true;   // 3xFP16 needs fp16-range w
+    if (!(std::fabs(k[i]) < 65504.0f / 256.0f)) c->loading_f16_bad = true;
   w->kh = kh;
   w->kw = kw;
   w->cin = cin;

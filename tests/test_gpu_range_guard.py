@@ -69,11 +69,13 @@ def test_od_activation_overflow_device_call_reports_range():
     assert c.range_check() == 0                   # reported once, then cleared
 
 
-def test_out_of_range_weights_run_exact_f32():
+@pytest.mark.parametrize('big', [300.0, 7.0e4])
+def test_out_of_range_weights_run_exact_f32(big):
+    """conv_h3 splits w * 2^8: |w| >= 65504 / 2^8 (= 255.9) already leaves the fp16 range"""
     from mmla_audio_amd import _lib, weights
     W = weights.synthetic(weights.OD, seed=6)
     W['layer_with_weights-20/kernel'] = W['layer_with_weights-20/kernel'].copy()
-    W['layer_with_weights-20/kernel'][0, 0, 0, 0] = 7.0e4     # block 5's 3x3 conv
+    W['layer_with_weights-20/kernel'][0, 0, 0, 0] = big      # block 5's 3x3 conv
     pcm = synth.batch(330, 6, 40000)
     c = _ctx(W_od=W)
     p, a, _ = c.od_pipeline(pcm)
