@@ -78,8 +78,25 @@ constexpr int EARLY_B_VGPRS = 168;
 
 // V4: channels loaded as float4 (cin % 4 == 0); else per element (the SI stem, cin = 39).
 // PIN (Conv1D): the input rows are MaxPool1D(2, 'same') of x, taken while staging (SI pool units)
+// Shape: the layer geometry, compile-time for the fixed OD-NET / SI-NET layers (every bound,
+// division and address offset folds) or read from the arguments (Shape<0, 0, 0, 0>)
+template <int SH, int SW, int SCI, int SCO>
+struct Shape {
+  static constexpr bool FIXED = SH > 0;
+};
+
+template <class S> struct ShapeOf;
+template <int SH, int SW, int SCI, int SCO>
+struct ShapeOf<Shape<SH, SW, SCI, SCO>> {
+  static constexpr int h = SH, w = SW, ci = SCI, co = SCO;
+};
+template <class S> MMLA_DEV constexpr int shp_h() { return ShapeOf<S>::h; }
+template <class S> MMLA_DEV constexpr int shp_w() { return ShapeOf<S>::w; }
+template <class S> MMLA_DEV constexpr int shp_ci() { return ShapeOf<S>::ci; }
+template <class S> MMLA_DEV constexpr int shp_co() { return ShapeOf<S>::co; }
+
 template <int KH, int KW, int CK, int BN, int TW, int PRO, int EPI, bool POOL, bool V4 = true,
-          bool PIN = false>
+          bool PIN = false, class SHP = Shape<0, 0, 0, 0>>
 __global__ void __launch_bounds__(NT, 2) conv_h3_kernel(ConvH3Args a) {
   // each wave owns ONE 32-column slice of B (no B fragment is loaded by two waves) and
   // 128 / WM rows: BN 32 -> 4 x 1, BN 64 -> 2 x 2, BN 128 -> 1 x 4 (waves along N)
@@ -105,16 +122,25 @@ __global__ void __launch_bounds__(NT, 2) conv_h3_kernel(ConvH3Args a) {
   __shared__ __attribute__((aligned(16))) _Float16 lds_lo[NPIX * LDP];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // layer geometry (compile-time when SHP is a fixed shape: cin, cout are then their padded sizes)
+  constexpr bool FX = SHP::FIXED;
+  const int A_H = FX ? shp_h<SHP>() : a.h, A_W = FX ? shp_w<SHP>() : a.w;
+  const int A_CIN = FX ? shp_ci<SHP>() : a.cin, A_COUT = FX ? shp_co<SHP>() : a.cout;
+  const int A_CINP = FX ? shp_ci<SHP>() : a.cin_pad, A_COUTP = FX ? shp_co<SHP>() : a.cout_pad;
+  const int A_PH = FX ? (KH - 1) / 2 : a.pad_h, A_PW = FX ? (KW - 1) / 2 : a.pad_w;
   const int wm = wave / WN, wn = wave - (wave / WN) * WN;
   // TW == 1 (Conv1D): the clips' rows form ONE sequence of n * h rows tiled 128 at a time, so a
   // short sequence (t = 64, 32) does not pad a tile; taps that cross a clip boundary read zeros
-  const int HH = TW <= 1 ? a.n * a.h : a.h;
-  const int tiles = a.tiles_h * a.tiles_w;
+  const int HH = TW <= 1 ? a.n * A_H : A_H;
+  // tiles per clip (TW > 1) / in total (LIN, Conv1D: tiles_w = 1)
+  const int TLW = TW <= 1 ? 1 : (FX ? (A_W + TW - 1) / (TW > 1 ? TW : 1) : a.tiles_w);
+  const int TLH = FX && TW > 1 ? (A_H + TH - 1) / (TH > 0 ? TH : 1) : a.tiles_h;
+  const int tiles = TLH * TLW;
   const int64_t clip = TW <= 1 ? 0 : blockIdx.x / tiles;
   const int tile = blockIdx.x - (int)(clip * tiles);
-  const int th_i = tile / a.tiles_w;
+  const int th_i = tile / TLW;
   const int h0 = th_i * TH;
-  const int w0 = (tile - th_i * a.tiles_w) * TW;
+  const int w0 = (tile - th_i * TLW) * TW;
   const int n0 = blockIdx.y * BN;
 
   int apix[MT];
@@ -125,23 +151,23 @@ __global__ void __launch_bounds__(NT, 2) conv_h3_kernel(ConvH3Args a) {
   }
   int trow[MT];   // TW == 1: the A row's position inside its clip
 #pragma unroll
-  for (int mt = 0; mt < MT; ++mt) trow[mt] = TW == 1 ? (h0 + (wm * MT + mt) * 32 + (lane & 31)) % a.h : 0;
+  for (int mt = 0; mt < MT; ++mt) trow[mt] = TW == 1 ? (h0 + (wm * MT + mt) * 32 + (lane & 31)) % A_H : 0;
   // LIN: p0 = first pixel of the tile (flattened over n * h * w), r0 = its row; per A row and
   // kernel row dy the LDS pixel of tap (dy, 0), or the zero row when the source row leaves the clip
-  const int wpad = a.w + KW - 1;
-  const int64_t npx = (int64_t)a.n * a.h * a.w;
+  const int wpad = A_W + KW - 1;
+  const int64_t npx = (int64_t)a.n * A_H * A_W;
   const int64_t p0 = LIN ? (int64_t)tile * BMK : 0;
-  const int r0 = LIN ? (int)(p0 / a.w) : 0;
+  const int r0 = LIN ? (int)(p0 / A_W) : 0;
   int abase[MT][LIN ? KH : 1];
   if constexpr (LIN) {
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
       const int64_t P = p0 + (wm * MT + mt) * 32 + (lane & 31);
-      const int r = (int)(P / a.w), c = (int)(P - (int64_t)r * a.w), cr = r % a.h;
+      const int r = (int)(P / A_W), c = (int)(P - (int64_t)r * A_W), cr = r % A_H;
 #pragma unroll
       for (int dy = 0; dy < KH; ++dy) {
-        const int sr = cr + dy - a.pad_h;
-        abase[mt][dy] = ((sr >= 0 && sr < a.h ? (r - r0 + dy) * wpad : LIN_SLOTS * wpad) + c) * LDP;
+        const int sr = cr + dy - A_PH;
+        abase[mt][dy] = ((sr >= 0 && sr < A_H ? (r - r0 + dy) * wpad : LIN_SLOTS * wpad) + c) * LDP;
       }
     }
     // the zero row (never staged)
@@ -165,21 +191,21 @@ __global__ void __launch_bounds__(NT, 2) conv_h3_kernel(ConvH3Args a) {
 #pragma unroll
   for (int nt = 0; nt < NTL; ++nt) {
     const int co = n0 + (wn * NTL + nt) * 32 + (lane & 31);
-    whp[nt] = a.wh + (size_t)co * a.cin_pad + koff;
-    wlp[nt] = a.wl + (size_t)co * a.cin_pad + koff;
+    whp[nt] = a.wh + (size_t)co * A_CINP + koff;
+    wlp[nt] = a.wl + (size_t)co * A_CINP + koff;
   }
-  const size_t tap_stride = (size_t)a.cout_pad * a.cin_pad;
+  const size_t tap_stride = (size_t)A_COUTP * A_CINP;
   // the epilogue's bias, loaded now: after the MFMA loop it cost a memory round trip of its own
   float bias_r[NTL];
 #pragma unroll
   for (int nt = 0; nt < NTL; ++nt) {
     const int co = n0 + (wn * NTL + nt) * 32 + (lane & 31);
-    if (EARLY_B) bias_r[nt] = co < a.cout ? a.bias[co] : 0.0f;
+    if (EARLY_B) bias_r[nt] = co < A_COUT ? a.bias[co] : 0.0f;
   }
-  const float* xclip = a.x + clip * HH * a.w * a.cin;
+  const float* xclip = a.x + clip * HH * A_W * A_CIN;
 
   bool rbad = false;   // 3xFP16 range guard: a staged operand left the fp16 range
-  const int nchunks = a.cin_pad / CK;
+  const int nchunks = A_CINP / CK;
   for (int ch = 0; ch < nchunks; ++ch) {
     const int ci0 = ch * CK;
     __syncthreads();   // every wave is done reading the previous chunk's halo
@@ -194,7 +220,7 @@ __global__ void __launch_bounds__(NT, 2) conv_h3_kernel(ConvH3Args a) {
     float4 psc = make_float4(0.f, 0.f, 0.f, 0.f), psh = psc;
     auto load_pro = [&]() {
       const int ci = ci0 + (tid % QPP) * 4;
-      if (PRO != PRO_NONE && ci < a.cin) {
+      if (PRO != PRO_NONE && ci < A_CIN) {
         psc = *reinterpret_cast<const float4*>(a.scale + ci);
         psh = *reinterpret_cast<const float4*>(a.shift + ci);
       }
@@ -209,17 +235,17 @@ __global__ void __launch_bounds__(NT, 2) conv_h3_kernel(ConvH3Args a) {
       if (task < nstg * QPP) {
         const int px = task / QPP, q = task % QPP;
         const int py = LIN ? px / wpad : px / WP, pxx = LIN ? px - py * wpad : px % WP;
-        const int ih = (LIN ? r0 : h0) - a.pad_h + py, iw = w0 - a.pad_w + pxx;
+        const int ih = (LIN ? r0 : h0) - A_PH + py, iw = w0 - A_PW + pxx;
         const int ci = ci0 + q * 4;
-        if (ih >= 0 && ih < HH && iw >= 0 && iw < a.w && ci < a.cin) {
-          const float* src = xclip + (ih * a.w + iw) * a.cin + ci;
+        if (ih >= 0 && ih < HH && iw >= 0 && iw < A_W && ci < A_CIN) {
+          const float* src = xclip + (ih * A_W + iw) * A_CIN + ci;
           if constexpr (PIN) {
             // pooled row ih = (clip, tt) <- unpooled rows 2 tt, 2 tt + 1 of that clip
-            const int cl = ih / a.h, tt = ih - cl * a.h;
-            src = a.x + ((int64_t)cl * a.h_in + 2 * tt) * a.cin + ci;
+            const int cl = ih / A_H, tt = ih - cl * A_H;
+            src = a.x + ((int64_t)cl * a.h_in + 2 * tt) * A_CIN + ci;
             float4 v = *reinterpret_cast<const float4*>(src);
             if (2 * tt + 1 < a.h_in) {
-              const float4 u = *reinterpret_cast<const float4*>(src + a.cin);
+              const float4 u = *reinterpret_cast<const float4*>(src + A_CIN);
               v = make_float4(fmaxf(v.x, u.x), fmaxf(v.y, u.y), fmaxf(v.z, u.z), fmaxf(v.w, u.w));
             }
             pre[j] = v;
@@ -227,9 +253,9 @@ __global__ void __launch_bounds__(NT, 2) conv_h3_kernel(ConvH3Args a) {
             pre[j] = *reinterpret_cast<const float4*>(src);
           } else {
             pre[j].x = src[0];
-            pre[j].y = ci + 1 < a.cin ? src[1] : 0.0f;
-            pre[j].z = ci + 2 < a.cin ? src[2] : 0.0f;
-            pre[j].w = ci + 3 < a.cin ? src[3] : 0.0f;
+            pre[j].y = ci + 1 < A_CIN ? src[1] : 0.0f;
+            pre[j].z = ci + 2 < A_CIN ? src[2] : 0.0f;
+            pre[j].w = ci + 3 < A_CIN ? src[3] : 0.0f;
           }
           valid |= 1u << j;
         }
@@ -310,8 +336,8 @@ __global__ void __launch_bounds__(NT, 2) conv_h3_kernel(ConvH3Args a) {
           f16x8 ah = *reinterpret_cast<const f16x8*>(lds_hi + off);
           f16x8 al = *reinterpret_cast<const f16x8*>(lds_lo + off);
           if constexpr (TW == 1 && KH > 1) {
-            const int src = trow[mt] + dy - a.pad_h;
-            if (src < 0 || src >= a.h) {
+            const int src = trow[mt] + dy - A_PH;
+            if (src < 0 || src >= A_H) {
               ah = f16x8{};
               al = f16x8{};
             }
@@ -353,18 +379,18 @@ __global__ void __launch_bounds__(NT, 2) conv_h3_kernel(ConvH3Args a) {
         for (int g = 0; g < 4; ++g) {
           const int m0 = mbase + 8 * g + hsel;
           if constexpr (LIN) {
-            const float* rp = a.res + (p0 + m0) * a.cout + co;
+            const float* rp = a.res + (p0 + m0) * A_COUT + co;
 #pragma unroll
             for (int j = 0; j < 4; ++j)
-              rsd[nt][mt][4 * g + j] = co < a.cout && p0 + m0 + j < npx ? rp[j * a.cout] : 0.0f;
+              rsd[nt][mt][4 * g + j] = co < A_COUT && p0 + m0 + j < npx ? rp[j * A_COUT] : 0.0f;
             continue;
           }
           const int oh = h0 + m0 / (LIN ? 1 : TW), ow0 = w0 + m0 % (LIN ? 1 : TW);
-          const float* rp = a.res + ((clip * HH + oh) * a.w + ow0) * a.cout + co;
+          const float* rp = a.res + ((clip * HH + oh) * A_W + ow0) * A_COUT + co;
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            const int step = TW == 1 ? a.w * a.cout : a.cout;
-            const bool ok = co < a.cout && oh < HH && (TW == 1 ? (oh + j < HH) : (ow0 + j < a.w));
+            const int step = TW == 1 ? A_W * A_COUT : A_COUT;
+            const bool ok = co < A_COUT && oh < HH && (TW == 1 ? (oh + j < HH) : (ow0 + j < A_W));
             rsd[nt][mt][4 * g + j] = ok ? rp[j * step] : 0.0f;
           }
         }
@@ -374,7 +400,7 @@ __global__ void __launch_bounds__(NT, 2) conv_h3_kernel(ConvH3Args a) {
 #pragma unroll
   for (int nt = 0; nt < NTL; ++nt) {
     const int co = n0 + (wn * NTL + nt) * 32 + (lane & 31);
-    if (co >= a.cout) continue;
+    if (co >= A_COUT) continue;
     const float b = EARLY_B ? bias_r[nt] : a.bias[co];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
@@ -387,7 +413,7 @@ __global__ void __launch_bounds__(NT, 2) conv_h3_kernel(ConvH3Args a) {
         // {4q+e, 4q+e+1, 4q+e+TW/2, 4q+e+TW/2+1}  (row + TW = register + TW/2)
         static_assert(TW == 16 || TW == 8, "pooled epilogue needs TW 8 or 16");
         constexpr int TWP = TW == 16 ? 16 : 8;
-        const int hp = (a.h + 1) >> 1, wp = (a.w + 1) >> 1;
+        const int hp = (A_H + 1) >> 1, wp = (A_W + 1) >> 1;
 #pragma unroll
         for (int q = 0; q < 4; ++q)
 #pragma unroll
@@ -398,39 +424,39 @@ __global__ void __launch_bounds__(NT, 2) conv_h3_kernel(ConvH3Args a) {
             if (4 * q + e + R + 1 > 15) continue;
             const int m = mbase + i;
             const int oh = h0 + m / TWP, ow = w0 + m % TWP;
-            if (oh >= a.h || ow >= a.w) continue;
+            if (oh >= A_H || ow >= A_W) continue;
             float mx = v[4 * q + e];
-            if (ow + 1 < a.w) mx = fmaxf(mx, v[4 * q + e + 1]);
-            if (oh + 1 < a.h) {
+            if (ow + 1 < A_W) mx = fmaxf(mx, v[4 * q + e + 1]);
+            if (oh + 1 < A_H) {
               mx = fmaxf(mx, v[4 * q + e + R]);
-              if (ow + 1 < a.w) mx = fmaxf(mx, v[4 * q + e + R + 1]);
+              if (ow + 1 < A_W) mx = fmaxf(mx, v[4 * q + e + R + 1]);
             }
-            a.y[((clip * hp + (oh >> 1)) * wp + (ow >> 1)) * a.cout + co] = mx;
+            a.y[((clip * hp + (oh >> 1)) * wp + (ow >> 1)) * A_COUT + co] = mx;
           }
       } else {
 #pragma unroll
         for (int g = 0; g < 4; ++g) {        // 4 groups of 4 consecutive tile rows
           const int m0 = mbase + 8 * g + hsel;
           if constexpr (LIN) {               // 4 consecutive pixels of the flattened batch
-            float* yp = a.y + (p0 + m0) * a.cout + co;
+            float* yp = a.y + (p0 + m0) * A_COUT + co;
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
               if (p0 + m0 + j >= npx) continue;
               float val = v[4 * g + j];
               if constexpr (EPI == EPI_ADD) val += rsd[nt][mt][4 * g + j];
-              yp[j * a.cout] = val;
+              yp[j * A_COUT] = val;
             }
             continue;
           }
           const int oh = h0 + m0 / (LIN ? 1 : TW);
           if (oh >= HH) continue;
           const int ow0 = w0 + m0 % (LIN ? 1 : TW);
-          float* yp = a.y + ((clip * HH + oh) * a.w + ow0) * a.cout + co;
+          float* yp = a.y + ((clip * HH + oh) * A_W + ow0) * A_COUT + co;
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             // TW >= 4 keeps the 4 rows in one image row; TW == 1 walks image rows instead
-            const int step = TW == 1 ? a.w * a.cout : a.cout;
-            const bool ok = TW == 1 ? (oh + j < HH) : (ow0 + j < a.w);
+            const int step = TW == 1 ? A_W * A_COUT : A_COUT;
+            const bool ok = TW == 1 ? (oh + j < HH) : (ow0 + j < A_W);
             if (!ok) continue;
             float val = v[4 * g + j];
             if constexpr (EPI == EPI_ADD) val += rsd[nt][mt][4 * g + j];
@@ -444,7 +470,7 @@ __global__ void __launch_bounds__(NT, 2) conv_h3_kernel(ConvH3Args a) {
 }
 
 template <int KH, int KW, int CK, int BN, int TW, int PRO, int EPI, bool POOL, bool V4 = true,
-          bool PIN = false>
+          bool PIN = false, class SHP = Shape<0, 0, 0, 0>>
 hipError_t launch(ConvH3Args a, hipStream_t s) {
   constexpr int BMK = tile_px<KH, BN, TW>();
   if constexpr (TW == 0) {
@@ -457,16 +483,17 @@ hipError_t launch(ConvH3Args a, hipStream_t s) {
   }
   const int64_t tiles = (int64_t)a.tiles_h * a.tiles_w * (TW <= 1 ? 1 : a.n);
   dim3 grid((unsigned)tiles, (unsigned)(a.cout_pad / BN));
-  hipLaunchKernelGGL((conv_h3_kernel<KH, KW, CK, BN, TW, PRO, EPI, POOL, V4, PIN>), grid, dim3(NT), 0,
-                     s, a);
+  hipLaunchKernelGGL((conv_h3_kernel<KH, KW, CK, BN, TW, PRO, EPI, POOL, V4, PIN, SHP>), grid,
+                     dim3(NT), 0, s, a);
   return hipGetLastError();
 }
 
-template <int KH, int KW, int CK, int TW, int PRO, int EPI, bool POOL, bool PIN = false>
+template <int KH, int KW, int CK, int TW, int PRO, int EPI, bool POOL, bool PIN = false,
+          class SHP = Shape<0, 0, 0, 0>>
 hipError_t by_bn(const ConvH3Args& a, hipStream_t s) {
-  if (a.cout_pad % 128 == 0) return launch<KH, KW, CK, 128, TW, PRO, EPI, POOL, true, PIN>(a, s);
-  if (a.cout_pad % 64 == 0) return launch<KH, KW, CK, 64, TW, PRO, EPI, POOL, true, PIN>(a, s);
-  return launch<KH, KW, CK, 32, TW, PRO, EPI, POOL, true, PIN>(a, s);
+  if (a.cout_pad % 128 == 0) return launch<KH, KW, CK, 128, TW, PRO, EPI, POOL, true, PIN, SHP>(a, s);
+  if (a.cout_pad % 64 == 0) return launch<KH, KW, CK, 64, TW, PRO, EPI, POOL, true, PIN, SHP>(a, s);
+  return launch<KH, KW, CK, 32, TW, PRO, EPI, POOL, true, PIN, SHP>(a, s);
 }
 
 }  // namespace
@@ -502,6 +529,26 @@ hipError_t conv_h3_launch(ConvH3Args a, hipStream_t s) {
       return by_bn<3, 1, 32, 1, PRO_BN_RELU, EPI_BIAS, false, true>(a, s);
     return hipErrorInvalidValue;
   }
+  // the fixed OD-NET layers (blocks 4-9 on the 128 x 151 image): compile-time geometry
+#ifndef CONV_H3_FIXED
+#define CONV_H3_FIXED 1
+#endif
+  const bool std_pad = CONV_H3_FIXED && a.pad_h == (a.kh - 1) / 2 && a.pad_w == (a.kw - 1) / 2 &&
+                       a.cin == a.cin_pad && a.cout == a.cout_pad;
+#define H3F(KH, KW, TW, E, PL, H, W, CI, CO)                                                     \
+  if (std_pad && a.kh == KH && a.kw == KW && ck == 32 && a.tw == TW && a.pro == PRO_BN_ELU &&   \
+      a.epi == E && (a.pool_out != 0) == PL && a.h == H && a.w == W && a.cin == CI &&          \
+      a.cout == CO)                                                                            \
+    return by_bn<KH, KW, 32, TW, PRO_BN_ELU, E, PL, false, Shape<H, W, CI, CO>>(a, s);
+  H3F(3, 3, 16, EPI_BIAS, false, 64, 76, 32, 64)     // block 4
+  H3F(4, 1, 16, EPI_BIAS, true, 64, 76, 64, 64)
+  H3F(3, 3, 8, EPI_BIAS, false, 32, 38, 64, 64)      // blocks 5-6
+  H3F(4, 1, 8, EPI_ADD, false, 32, 38, 64, 64)
+  H3F(3, 3, 8, EPI_BIAS, false, 32, 38, 64, 128)     // block 7
+  H3F(4, 1, 8, EPI_BIAS, true, 32, 38, 128, 128)
+  H3F(3, 3, 0, EPI_BIAS, false, 16, 19, 128, 128)    // blocks 8-9
+  // (blocks 8-9 conv(4,1) + residual: the fixed-shape build was slower, 3.0 -> 3.3 ms)
+#undef H3F
 #define H3(KH, KW, CK, TW, P, E, PL)                                                           \
   if (a.kh == KH && a.kw == KW && ck == CK && a.tw == TW && a.pro == P && a.epi == E &&        \
       (a.pool_out != 0) == PL)                                                                 \
