@@ -7,7 +7,7 @@
 struct ConvH3Args {
   const float* x;        // [N, H, W, Cin] float32 NHWC
   const uint16_t* wh;    // [KH*KW][CoutPad][CinPad] fp16 hi(w)
-  const uint16_t* wl;    // [KH*KW][CoutPad][CinPad] fp16 lo(w) = fp16((w - hi) * 2^11)
+  const uint16_t* wl;    // [KH*KW][CoutPad][CinPad] fp16 lo = fp16(w * 2^8 - hi), hi = fp16(w * 2^8)
   const float* bias;     // [CoutPad]
   const float* scale;    // [Cin] prologue BN scale (nullable when pro == 0)
   const float* shift;    // [Cin]

@@ -6,7 +6,7 @@
 struct ResBlkArgs {
   const float* x;          // [N, H, W, CIN] block input (raw: also the residual of non-pool blocks)
   const uint16_t* w1h;     // Conv2D(3x3) fp16 hi [C][K1PAD], k = (dy * 3 + dx) * CIN + ci
-  const uint16_t* w1l;     //                 lo = fp16((w - hi) * 2^11)
+  const uint16_t* w1l;     //                 lo = fp16(w * 2^8 - hi), hi = fp16(w * 2^8)
   const float* b1;         // [C]
   const float* s1;         // BatchNorm before the 3x3 conv, folded: y = x * s1 + t1   [CIN]
   const float* t1;

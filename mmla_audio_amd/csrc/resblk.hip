@@ -19,7 +19,8 @@
 // A[row l & 15][k 8 (l >> 4) .. +7] (one ds_read_b128 per operand half), B[k 8 (l >> 4) .. +7][col
 // l & 15] (one 16-B global load from the [C][K] weight image) and C[rows 4 (l >> 4) .. +3][col l & 15].
 // K runs over (tap, channel) with the channel fastest, so CIN = 16 packs two taps per k-step.
-// 3xFP16: acc1 += hi*hi, acc2 += hi*lo + lo*hi; value = acc1 + 2^-11 acc2 (see conv_h3.hip).
+// 3xFP16 as in conv_h3.hip: activations x 2^4 and weights x 2^8 split into hi + lo (lo unscaled),
+// ONE accumulator per tile: acc += hi*hi + hi*lo + lo*hi; value = acc * 2^-12.
 #include "resblk.h"
 
 #ifndef RB_EXP
@@ -49,8 +50,10 @@ typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 constexpr int NT = 256;
 constexpr int TW = 16;
 constexpr int TH = 16;
-constexpr float LO_SCALE = 2048.0f;
-constexpr float LO_INV = 1.0f / 2048.0f;
+constexpr float ACT_SCALE = 16.0f;     // 2^4: every split activation
+constexpr float W_SCALE = 256.0f;      // 2^8: weights (resblk_split_weights)
+constexpr float UNSCALE = 1.0f / (ACT_SCALE * W_SCALE);
+constexpr float ACT_RANGE = 65504.0f / ACT_SCALE;
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
@@ -64,17 +67,19 @@ __device__ __forceinline__ f32x2 elu2(f32x2 u) {
   return f32x2{u.x > 0.0f ? u.x : e.x, u.y > 0.0f ? u.y : e.y};
 }
 
-// v = hi + 2^-11 lo, both fp16 (RNE)
+// v * 2^4 = hi + lo, both fp16 (RNE)
 __device__ __forceinline__ void split2(f32x2 v, f16x2& h, f16x2& l) {
+  v = v * ACT_SCALE;
   h = __builtin_convertvector(v, f16x2);
   const f32x2 hf = __builtin_convertvector(h, f32x2);
-  l = __builtin_convertvector((v - hf) * LO_SCALE, f16x2);
+  l = __builtin_convertvector(v - hf, f16x2);
 }
 
 // the 3 channels of image pixel `pix` (uint8 decoded PNG or float NHWC), as floats
-// 3xFP16 range guard: false when a value about to be split is >= 65504 in magnitude (or inf)
+// 3xFP16 range guard: false when a value about to be split leaves the fp16 range once scaled
+// (|v| >= 65504 / 2^4) or is not finite
 __device__ __forceinline__ bool in_f16_range(f32x2 a, f32x2 b) {
-  return fmaxf(fmaxf(fabsf(a.x), fabsf(a.y)), fmaxf(fabsf(b.x), fabsf(b.y))) < 65504.0f;
+  return fmaxf(fmaxf(fabsf(a.x), fabsf(a.y)), fmaxf(fabsf(b.x), fabsf(b.y))) < ACT_RANGE;
 }
 
 __device__ __forceinline__ float4 image_px(const ResBlkArgs& a, int64_t pix) {
@@ -219,7 +224,7 @@ __global__ void __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(R
   constexpr int KSC = POOL ? G::KSC : 1;
   float4 scx[KSC][MSC][2];
   f16x8 scbh[KSC][NTW], scbl[KSC][NTW];
-  f32x4 e1[MSC][NTW], e2[MSC][NTW];
+  f32x4 e1[MSC][NTW];
   if constexpr (POOL) {
     const int p = col;                            // this lane's A row (pooled pixel of the tile)
     const int pr = (p & 3) >> 1, pc = 2 * (p >> 2) + (p & 1);
@@ -319,7 +324,6 @@ __global__ void __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(R
 #pragma unroll
       for (int nt = 0; nt < NTW; ++nt) {
         e1[j][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-        e2[j][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
       }
 #pragma unroll
     for (int s = 0; s < KSC; ++s)
@@ -337,22 +341,19 @@ __global__ void __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(R
         const f16x8 al = {l0_.x, l0_.y, l1_.x, l1_.y, l2_.x, l2_.y, l3_.x, l3_.y};
 #pragma unroll
         for (int nt = 0; nt < NTW; ++nt) {
+          e1[j][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, scbl[s][nt], e1[j][nt], 0, 0, 0);
+          e1[j][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, scbh[s][nt], e1[j][nt], 0, 0, 0);
           e1[j][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, scbh[s][nt], e1[j][nt], 0, 0, 0);
-          e2[j][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, scbl[s][nt], e2[j][nt], 0, 0, 0);
-          e2[j][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, scbh[s][nt], e2[j][nt], 0, 0, 0);
         }
       }
   }
   RB_MARK(2);
   // ---- GEMM 1: t1 rows [wm * MT1, +MT1) x this wave's N tiles, K = (tap, ci) ----------------------
-  f32x4 acc1[MT1][NTW], acc2[MT1][NTW];
+  f32x4 acc1[MT1][NTW];
 #pragma unroll
   for (int m = 0; m < MT1; ++m)
 #pragma unroll
-    for (int nt = 0; nt < NTW; ++nt) {
-      acc1[m][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-      acc2[m][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
+    for (int nt = 0; nt < NTW; ++nt) acc1[m][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
   {
     const _Float16* ahb = smem + (wm * MT1 * XC + col) * XPS;   // + m * XC * XPS (immediate)
     const _Float16* alb = ahb + G::XLO;
@@ -384,13 +385,12 @@ __global__ void __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(R
 #pragma unroll
         for (int nt = 0; nt < NTW; ++nt) {
 #if RB_EXP == 2
-          acc1[m][nt][0] += (float)ah[0] * (float)ch[nt][0];
-          acc2[m][nt][0] += (float)al[0] * (float)cl[nt][0];
+          acc1[m][nt][0] += (float)ah[0] * (float)ch[nt][0] + (float)al[0] * (float)cl[nt][0];
           continue;
 #endif
+          acc1[m][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, cl[nt], acc1[m][nt], 0, 0, 0);
+          acc1[m][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, ch[nt], acc1[m][nt], 0, 0, 0);
           acc1[m][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, ch[nt], acc1[m][nt], 0, 0, 0);
-          acc2[m][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, cl[nt], acc2[m][nt], 0, 0, 0);
-          acc2[m][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, ch[nt], acc2[m][nt], 0, 0, 0);
         }
       }
       __builtin_amdgcn_sched_barrier(0);   // keep the scheduler's LDS-read hoisting within a k-step
@@ -401,7 +401,7 @@ __global__ void __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(R
   RB_MARK(4);
 
   // ---- t1 -> LDS: BN2(acc + b1) + ELU; rows outside the image are the (4,1) conv's zero padding ----
-  // BN2(v + b1) = acc1 * s2 + acc2 * (2^-11 s2) + (b1 s2 + t2): two v_pk_fma_f32 per pixel pair
+  // BN2(v + b1) = acc * (2^-12 s2) + (b1 s2 + t2): one v_pk_fma_f32 per pixel pair
   {
     _Float16* const thb = smem + wm * MT1 * TW * TPS + 4 * grp * TPS;   // + (m * TW + i) * TPS + n
     _Float16* const tlb = thb + G::TLO;
@@ -410,7 +410,7 @@ __global__ void __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(R
       const int n = (wn * NTW + nt) * 16 + col;
       const float s2 = ps2[nt];
       const float c2 = fmaf(pb1[nt], s2, pt2[nt]);
-      const f32x2 s2v = {s2, s2}, s2l = {s2 * LO_INV, s2 * LO_INV}, c2v = {c2, c2};
+      const f32x2 s2v = {s2 * UNSCALE, s2 * UNSCALE}, c2v = {c2, c2};
 #pragma unroll
       for (int m = 0; m < MT1; ++m) {
         const int ih = h0 - 1 + wm * MT1 + m;   // scalar
@@ -421,12 +421,11 @@ __global__ void __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(R
         for (int i = 0; i < 4; i += 2) {
 #if RB_EXP == 3
           thb[(m * TW + i) * TPS + n] = (_Float16)(acc1[m][nt][i] * rm);
-          tlb[(m * TW + i) * TPS + n] = (_Float16)(acc2[m][nt][i + 1] * rm);
+          tlb[(m * TW + i) * TPS + n] = (_Float16)(acc1[m][nt][i + 1] * rm);
           continue;
 #endif
           const f32x2 x1 = {acc1[m][nt][i], acc1[m][nt][i + 1]};
-          const f32x2 x2 = {acc2[m][nt][i], acc2[m][nt][i + 1]};
-          const f32x2 u = elu2(x1 * s2v + (x2 * s2l + c2v));
+          const f32x2 u = elu2(x1 * s2v + c2v);
           // guard only the live t1 rows: the padding rows (>= TR, and outside the image) hold
           // whatever GEMM 1 made of unstaged LDS and are multiplied by 0 / never read
           rbad |= rm != 0.0f && wm * MT1 + m < G::TR && !in_f16_range(u, u);
@@ -445,14 +444,11 @@ __global__ void __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(R
 
   RB_MARK(5);
   // ---- GEMM 2: output rows [wm * MT2, +MT2), K = (dy, ci) over t1 rows r + dy --------------------
-  f32x4 d1[MT2][NTW], d2[MT2][NTW];
+  f32x4 d1[MT2][NTW];
 #pragma unroll
   for (int m = 0; m < MT2; ++m)
 #pragma unroll
-    for (int nt = 0; nt < NTW; ++nt) {
-      d1[m][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-      d2[m][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
+    for (int nt = 0; nt < NTW; ++nt) d1[m][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
   {
     const _Float16* ahb = smem + (wm * MT2 * TW + col) * TPS;
     const _Float16* alb = ahb + G::TLO;
@@ -481,13 +477,12 @@ __global__ void __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(R
 #pragma unroll
         for (int nt = 0; nt < NTW; ++nt) {
 #if RB_EXP == 2
-          d1[m][nt][0] += (float)ah[0] * (float)gh[nt][0];
-          d2[m][nt][0] += (float)al[0] * (float)gl[nt][0];
+          d1[m][nt][0] += (float)ah[0] * (float)gh[nt][0] + (float)al[0] * (float)gl[nt][0];
           continue;
 #endif
+          d1[m][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, gl[nt], d1[m][nt], 0, 0, 0);
+          d1[m][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, gh[nt], d1[m][nt], 0, 0, 0);
           d1[m][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, gh[nt], d1[m][nt], 0, 0, 0);
-          d2[m][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, gl[nt], d2[m][nt], 0, 0, 0);
-          d2[m][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, gh[nt], d2[m][nt], 0, 0, 0);
         }
       }
       __builtin_amdgcn_sched_barrier(0);
@@ -511,17 +506,17 @@ __global__ void __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(R
           const int m = 4 * j + 2 * (i >> 1);        // t2 row pair (m, m + 1) of this wave
           const int e = 2 * (i & 1);                  // column pair (e, e + 1) of the lane's 4
           const int oh = h0 + wm * MT2 + m, ow = w0 + 4 * grp + e;   // even
-          float mx = d1[m][nt][e] + d2[m][nt][e] * LO_INV;
-          float v01 = d1[m][nt][e + 1] + d2[m][nt][e + 1] * LO_INV;
-          float v10 = d1[m + 1][nt][e] + d2[m + 1][nt][e] * LO_INV;
-          float v11 = d1[m + 1][nt][e + 1] + d2[m + 1][nt][e + 1] * LO_INV;
+          float mx = d1[m][nt][e] * UNSCALE;
+          float v01 = d1[m][nt][e + 1] * UNSCALE;
+          float v10 = d1[m + 1][nt][e] * UNSCALE;
+          float v11 = d1[m + 1][nt][e + 1] * UNSCALE;
           if (!interior) {   // MaxPool2D 'same' on odd sizes: the window is cut at the edge
             if (oh >= a.h || ow >= a.w) continue;
             if (ow + 1 >= a.w) { v01 = mx; v11 = v10; }
             if (oh + 1 >= a.h) { v10 = mx; v11 = v01; }
           }
           mx = fmaxf(fmaxf(mx, v01), fmaxf(v10, v11));
-          const float sc = e1[j][nt][i] + e2[j][nt][i] * LO_INV;
+          const float sc = e1[j][nt][i] * UNSCALE;
           a.y[(((int64_t)clip * hp + (oh >> 1)) * wp + (ow >> 1)) * C + n] = mx + sc + b;
         }
     }
@@ -557,7 +552,7 @@ __global__ void __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(R
         for (int i = 0; i < 4; ++i) {
           if (!interior && w0 + 4 * grp + i >= a.w) continue;
           const int64_t o = (rowbase + i) * C + n;
-          a.y[o] = d1[m][nt][i] + d2[m][nt][i] * LO_INV + b + rsd[nt][m][i];
+          a.y[o] = fmaf(d1[m][nt][i], UNSCALE, b) + rsd[nt][m][i];
         }
       }
     }
@@ -613,10 +608,10 @@ void resblk_split_weights(const float* w, int taps, int cin, int cout, int kpad,
   for (int t = 0; t < taps; ++t)
     for (int ci = 0; ci < cin; ++ci)
       for (int co = 0; co < cout; ++co) {
-        const float v = w[((size_t)t * cin + ci) * cout + co];
+        const float v = w[((size_t)t * cin + ci) * cout + co] * W_SCALE;   // exact
         const _Float16 h = (_Float16)v;
         const size_t o = (size_t)co * kpad + (size_t)t * cin + ci;
         hi[o] = f16_bits(v);
-        lo[o] = f16_bits((v - (float)h) * LO_SCALE);
+        lo[o] = f16_bits(v - (float)h);
       }
 }
