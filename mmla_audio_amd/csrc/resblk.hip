@@ -490,11 +490,19 @@ __global__ void __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(R
   }
 
   RB_MARK(6);
-  // ---- epilogue ------------------------------------------------------------------------------------
+  // ---- epilogue through LDS: the tile's outputs go to LDS as f32 [pixel][C + 4] (the 4-dword pad
+  //      puts the four lane groups of a ds_write_b32 on distinct banks), then every thread writes
+  //      whole 16-B channel quads of consecutive pixels: 2 (pool) / 8 fully coalesced dwordx4 stores
+  //      per thread instead of 8 / 32 dword stores per lane (and, non-pool, no residual loads: the
+  //      residual is the raw halo interior this thread staged, still in pre[]) --------------------
+  constexpr int OPS = C + 4;
+  float* const so = reinterpret_cast<float*>(smem);
+  static_assert(TH * TW * OPS * 2 <= G::SM, "the output tile fits the halo / t1 bytes");
   const bool interior = h0 + TH <= a.h && w0 + TW <= a.w;   // scalar: no per-element bounds checks
+  __syncthreads();   // every wave is done reading t1 (GEMM 2)
   if constexpr (POOL) {
     constexpr int MSC = MT2 / 4;
-    const int hp = (a.h + 1) >> 1, wp = (a.w + 1) >> 1;
+    constexpr int PW = TW / 2;                                   // pooled tile: PW x PW pixels
 #pragma unroll
     for (int nt = 0; nt < NTW; ++nt) {
       const int n = (wn * NTW + nt) * 16 + col;
@@ -517,44 +525,48 @@ __global__ void __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(R
           }
           mx = fmaxf(fmaxf(mx, v01), fmaxf(v10, v11));
           const float sc = e1[j][nt][i] * UNSCALE;
-          a.y[(((int64_t)clip * hp + (oh >> 1)) * wp + (ow >> 1)) * C + n] = mx + sc + b;
+          so[(((wm * MT2 + m) >> 1) * PW + ((4 * grp + e) >> 1)) * OPS + n] = mx + sc + b;
         }
+    }
+    __syncthreads();
+    const int hp = (a.h + 1) >> 1, wp = (a.w + 1) >> 1;
+    constexpr int QO = C / 4;                                    // float4 per output pixel
+#pragma unroll
+    for (int k = 0; k < (PW * PW * QO + NT - 1) / NT; ++k) {
+      const int idx = tid + k * NT;
+      if (idx >= PW * PW * QO) continue;
+      const int p = idx / QO, qq = idx - (idx / QO) * QO;
+      const int ph = (h0 >> 1) + p / PW, pw = (w0 >> 1) + p % PW;
+      if (!interior && (ph >= hp || pw >= wp)) continue;
+      *reinterpret_cast<float4*>(a.y + (((int64_t)clip * hp + ph) * wp + pw) * C + 4 * qq) =
+          *reinterpret_cast<const float4*>(so + p * OPS + 4 * qq);
     }
   } else {
-    // all of the lane's residual loads are issued before its first store: y and x are distinct
-    // buffers, but the compiler cannot know that, and a load it may not hoist above the previous
-    // store waits a full memory latency per element
-    float rsd[NTW][MT2][4];
-#pragma unroll
-    for (int nt = 0; nt < NTW; ++nt) {
-      const int n = (wn * NTW + nt) * 16 + col;
-#pragma unroll
-      for (int m = 0; m < MT2; ++m) {
-        // clamped into the image, loaded unconditionally (a static load count, no branches)
-        const int oh = min(h0 + wm * MT2 + m, a.h - 1);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int ow = min(w0 + 4 * grp + i, a.w - 1);
-          rsd[nt][m][i] = a.x[(((int64_t)clip * a.h + oh) * a.w + ow) * C + n];
-        }
-      }
-    }
+    static_assert(CIN == C, "the residual is the block input");
 #pragma unroll
     for (int nt = 0; nt < NTW; ++nt) {
       const int n = (wn * NTW + nt) * 16 + col;
       const float b = pbo[nt];
 #pragma unroll
-      for (int m = 0; m < MT2; ++m) {
-        const int oh = h0 + wm * MT2 + m;
-        if (!interior && oh >= a.h) continue;
-        const int64_t rowbase = ((int64_t)clip * a.h + oh) * a.w + w0 + 4 * grp;
+      for (int m = 0; m < MT2; ++m)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          if (!interior && w0 + 4 * grp + i >= a.w) continue;
-          const int64_t o = (rowbase + i) * C + n;
-          a.y[o] = fmaf(d1[m][nt][i], UNSCALE, b) + rsd[nt][m][i];
-        }
-      }
+        for (int i = 0; i < 4; ++i)
+          so[((wm * MT2 + m) * TW + 4 * grp + i) * OPS + n] = fmaf(d1[m][nt][i], UNSCALE, b);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < MAXT; ++j) {
+      const int px = (tid + j * NT) / QPP;
+      if (px >= G::XNP) continue;
+      const int py = px / XC, pxx = px - (px / XC) * XC;
+      const int r = py - 2, c = pxx - 1;                         // the halo pixel's output pixel
+      if (r < 0 || r >= TH || c < 0 || c >= TW) continue;
+      const int oh = h0 + r, ow = w0 + c;
+      if (!interior && (oh >= a.h || ow >= a.w)) continue;
+      const float4 v = *reinterpret_cast<const float4*>(so + (r * TW + c) * OPS + 4 * q);
+      const float4 x = pre[j];
+      *reinterpret_cast<float4*>(a.y + (((int64_t)clip * a.h + oh) * a.w + ow) * C + 4 * q) =
+          make_float4(v.x + x.x, v.y + x.y, v.z + x.z, v.w + x.w);
     }
   }
   RB_MARK(7);
