@@ -118,6 +118,14 @@ __global__ void __launch_bounds__(NT, 2) conv_h3_kernel(ConvH3Args a) {
   constexpr int MAXT = (NSTG * QPP + NT - 1) / NT;     // staged float4 per thread and chunk
   // registers allow the early loads (tap 0's B, prologue and epilogue parameters): EARLY_B_VGPRS
   constexpr bool EARLY_B = MT * NTL * 16 + MAXT * 4 + NTL * KS * 8 <= EARLY_B_VGPRS;
+  // CIL (channels in lane): the MFMA computes the transposed tile, so a lane holds 4 consecutive
+  // output channels of one pixel per register quad and the epilogue reads residuals and writes
+  // outputs as 16-B vectors (4x fewer memory instructions than one dword per (pixel, channel), but
+  // each instruction touches 32 pixels' 32-B pieces instead of two 128-B rows).  Measured per
+  // variant (rocprof A/B): only the 8-wide residual conv(4,1) gains (blocks 5-6: 4.43 -> 4.13 ms);
+  // the 3x3 and linear-pixel variants lose 2.5-6.6 % and the SI Conv1D stack 5 %.  The pooled
+  // epilogue needs the pixel-row layout (its 2x2 windows inside one lane's registers).
+  constexpr bool CIL = !POOL && EPI == EPI_ADD && TW == 8;
   __shared__ __attribute__((aligned(16))) _Float16 lds_hi[NPIX * LDP];
   __shared__ __attribute__((aligned(16))) _Float16 lds_lo[NPIX * LDP];
 
@@ -200,7 +208,7 @@ __global__ void __launch_bounds__(NT, 2) conv_h3_kernel(ConvH3Args a) {
 #pragma unroll
   for (int nt = 0; nt < NTL; ++nt) {
     const int co = n0 + (wn * NTL + nt) * 32 + (lane & 31);
-    if (EARLY_B) bias_r[nt] = co < A_COUT ? a.bias[co] : 0.0f;
+    if (EARLY_B && !CIL) bias_r[nt] = co < A_COUT ? a.bias[co] : 0.0f;
   }
   const float* xclip = a.x + clip * HH * A_W * A_CIN;
 
@@ -344,9 +352,15 @@ __global__ void __launch_bounds__(NT, 2) conv_h3_kernel(ConvH3Args a) {
           }
 #pragma unroll
           for (int nt = 0; nt < NTL; ++nt) {
-            acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl[nt][s], acc[mt][nt], 0, 0, 0);
-            acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[nt][s], acc[mt][nt], 0, 0, 0);
-            acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[nt][s], acc[mt][nt], 0, 0, 0);
+            if constexpr (CIL) {   // C^T: rows = channels, columns = pixels
+              acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(bl[nt][s], ah, acc[mt][nt], 0, 0, 0);
+              acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(bh[nt][s], al, acc[mt][nt], 0, 0, 0);
+              acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(bh[nt][s], ah, acc[mt][nt], 0, 0, 0);
+            } else {
+              acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl[nt][s], acc[mt][nt], 0, 0, 0);
+              acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[nt][s], acc[mt][nt], 0, 0, 0);
+              acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[nt][s], acc[mt][nt], 0, 0, 0);
+            }
           }
         }
       }
@@ -363,6 +377,67 @@ __global__ void __launch_bounds__(NT, 2) conv_h3_kernel(ConvH3Args a) {
   }
 
   // ---- epilogue ----------------------------------------------------------------------------------
+  if constexpr (CIL) {
+    // lane's register quad g holds channels 8 g + 4 (lane >> 5) + 0..3 of tile pixel
+    // mbase + (lane & 31); the pixel's output address for every (layout) case
+    auto pix_off = [&](int m, bool& ok) -> int64_t {
+      if constexpr (LIN) {
+        ok = p0 + m < npx;
+        return (p0 + m) * A_COUT;
+      } else {
+        const int oh = h0 + m / (TW > 1 ? TW : 1), ow = w0 + m % (TW > 1 ? TW : 1);
+        ok = oh < HH && ow < A_W;
+        return ((clip * HH + oh) * A_W + ow) * A_COUT;
+      }
+    };
+    const int cq = 4 * (lane >> 5);
+    // the in-place residual: every load issued before the first store (see the pixel-row path)
+    float4 rsd4[NTL][MT][4];
+    if constexpr (EPI == EPI_ADD) {
+#pragma unroll
+      for (int nt = 0; nt < NTL; ++nt)
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+          bool ok;
+          const int64_t o = pix_off((wm * MT + mt) * 32 + (lane & 31), ok);
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const int co = n0 + (wn * NTL + nt) * 32 + 8 * g + cq;
+            rsd4[nt][mt][g] = ok && co < A_COUT ? *reinterpret_cast<const float4*>(a.res + o + co)
+                                                 : make_float4(0.f, 0.f, 0.f, 0.f);
+          }
+        }
+    }
+#pragma unroll
+    for (int nt = 0; nt < NTL; ++nt) {
+      float4 b4[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int co = n0 + (wn * NTL + nt) * 32 + 8 * g + cq;
+        b4[g] = co < A_COUT ? *reinterpret_cast<const float4*>(a.bias + co) : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        bool ok;
+        const int64_t o = pix_off((wm * MT + mt) * 32 + (lane & 31), ok);
+        if (!ok) continue;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int co = n0 + (wn * NTL + nt) * 32 + 8 * g + cq;
+          if (co >= A_COUT) continue;
+          float4 v = make_float4(fmaf(acc[mt][nt][4 * g], UNSCALE, b4[g].x),
+                                 fmaf(acc[mt][nt][4 * g + 1], UNSCALE, b4[g].y),
+                                 fmaf(acc[mt][nt][4 * g + 2], UNSCALE, b4[g].z),
+                                 fmaf(acc[mt][nt][4 * g + 3], UNSCALE, b4[g].w));
+          if constexpr (EPI == EPI_ADD) {
+            const float4 r = rsd4[nt][mt][g];
+            v = make_float4(v.x + r.x, v.y + r.y, v.z + r.z, v.w + r.w);
+          }
+          *reinterpret_cast<float4*>(a.y + o + co) = v;
+        }
+      }
+    }
+  } else {
   // lane's accumulator register r holds tile row m = mbase + (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
   const int hsel = 4 * (lane >> 5);
   // the residual is added in place (res == y): all of the lane's residual loads are issued before
@@ -466,6 +541,7 @@ __global__ void __launch_bounds__(NT, 2) conv_h3_kernel(ConvH3Args a) {
       }
     }
   }
+  }   // CIL
   if (rbad && a.range_flag) *a.range_flag = 1;
 }
 
