@@ -625,6 +625,7 @@ hipError_t conv_h3_launch(ConvH3Args a, hipStream_t s) {
   H3F(3, 3, 0, EPI_BIAS, false, 16, 19, 128, 128)    // blocks 8-9
   // (blocks 8-9 conv(4,1) + residual: the fixed-shape build was slower, 3.0 -> 3.3 ms)
 #undef H3F
+  // (the SI Conv1D layers gained nothing from a fixed geometry: 48.3 vs 48.1 ms per step, A/B)
 #define H3(KH, KW, CK, TW, P, E, PL)                                                           \
   if (a.kh == KH && a.kw == KW && ck == CK && a.tw == TW && a.pro == P && a.epi == E &&        \
       (a.pool_out != 0) == PL)                                                                 \

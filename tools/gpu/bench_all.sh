@@ -4,16 +4,16 @@
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 900 python3 bench.py > gpurun_out/bench_od.json.log 2>&1 || exit $?
+timeout -k 10 900 python3 -u bench.py > gpurun_out/bench_od.json.log 2>&1 || exit $?
 grep '^{' gpurun_out/bench_od.json.log > gpurun_out/bench_od.json
-timeout -k 10 600 python3 bench.py --workload si_pipeline > gpurun_out/bench_si.json.log 2>&1 || exit $?
+timeout -k 10 600 python3 -u bench.py --workload si_pipeline > gpurun_out/bench_si.json.log 2>&1 || exit $?
 grep '^{' gpurun_out/bench_si.json.log > gpurun_out/bench_si.json
-timeout -k 10 600 python3 bench.py --workload od_features > gpurun_out/bench_fe.json.log 2>&1 || exit $?
+timeout -k 10 600 python3 -u bench.py --workload od_features > gpurun_out/bench_fe.json.log 2>&1 || exit $?
 grep '^{' gpurun_out/bench_fe.json.log > gpurun_out/bench_fe.json
-timeout -k 10 600 python3 bench.py --workload noise_gate > gpurun_out/bench_nr.json.log 2>&1 || exit $?
+timeout -k 10 600 python3 -u bench.py --workload noise_gate > gpurun_out/bench_nr.json.log 2>&1 || exit $?
 grep '^{' gpurun_out/bench_nr.json.log > gpurun_out/bench_nr.json
 rm -rf gpurun_out/prof_bench
-timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_bench -o od -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/prof_bench.log 2>&1 || exit $?
+timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_bench -o od -- python3 -u bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/prof_bench.log 2>&1 || exit $?
 python3 - <<'PY'
 import json
 for f in ('od', 'si', 'fe', 'nr'):
