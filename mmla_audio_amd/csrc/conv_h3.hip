@@ -33,6 +33,17 @@
 
 #include <cstring>
 
+#ifndef CH_EXP
+#define CH_EXP 0   // 1: s_memtime phase timeline of one selected launch (dev build, tools/ch_timeline.py)
+#endif
+#if CH_EXP
+// selection (kh, kw, h, cin, cout) and per-(workgroup, wave) phase sums of the first 8192
+// workgroups of blockIdx.y == 0: [prologue, stage, barrier, taps, epilogue, total, chunks, 0]
+__device__ int g_ch_sel[5];
+__device__ unsigned long long g_ch_t[8192 * 4 * 8];
+#define CH_T() __builtin_amdgcn_s_memtime()
+#endif
+
 namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -130,6 +141,11 @@ __global__ void __launch_bounds__(NT, 2) conv_h3_kernel(ConvH3Args a) {
   __shared__ __attribute__((aligned(16))) _Float16 lds_lo[NPIX * LDP];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+#if CH_EXP
+  const unsigned long long ch_t0 = CH_T();
+  unsigned long long ch_sum[5] = {0, 0, 0, 0, 0}, ch_a = 0, ch_b = 0, ch_c = 0;
+  int ch_n = 0;
+#endif
   // layer geometry (compile-time when SHP is a fixed shape: cin, cout are then their padded sizes)
   constexpr bool FX = SHP::FIXED;
   const int A_H = FX ? shp_h<SHP>() : a.h, A_W = FX ? shp_w<SHP>() : a.w;
@@ -284,6 +300,11 @@ __global__ void __launch_bounds__(NT, 2) conv_h3_kernel(ConvH3Args a) {
     };
     if constexpr (EARLY_B) load_b0();
     else load_pro();
+#if CH_EXP
+    ch_a = CH_T();
+    if (ch == 0) ch_sum[0] = ch_a - ch_t0;
+    else ch_sum[3] += ch_a - ch_c;   // the previous chunk's taps + this chunk's barrier and loads
+#endif
 #pragma unroll
     for (int j = 0; j < MAXT; ++j) {
       const int task = tid + j * NT;
@@ -316,7 +337,15 @@ __global__ void __launch_bounds__(NT, 2) conv_h3_kernel(ConvH3Args a) {
       *reinterpret_cast<f16x4*>(lds_hi + px * LDP + q * 4) = hv;
       *reinterpret_cast<f16x4*>(lds_lo + px * LDP + q * 4) = lv;
     }
+#if CH_EXP
+    ch_b = CH_T();
+    ch_sum[1] += ch_b - ch_a;
+#endif
     __syncthreads();
+#if CH_EXP
+    ch_c = CH_T();
+    ch_sum[2] += ch_c - ch_b;
+#endif
 
     // ---- all taps of this chunk ------------------------------------------------------------------
     if constexpr (!EARLY_B) load_b0();
@@ -376,6 +405,11 @@ __global__ void __launch_bounds__(NT, 2) conv_h3_kernel(ConvH3Args a) {
     }
   }
 
+#if CH_EXP
+  ch_b = CH_T();
+  ch_sum[3] += ch_b - ch_c;
+  ch_n = nchunks;
+#endif
   // ---- epilogue ----------------------------------------------------------------------------------
   if constexpr (CIL) {
     // lane's register quad g holds channels 8 g + 4 (lane >> 5) + 0..3 of tile pixel
@@ -543,6 +577,23 @@ __global__ void __launch_bounds__(NT, 2) conv_h3_kernel(ConvH3Args a) {
   }
   }   // CIL
   if (rbad && a.range_flag) *a.range_flag = 1;
+#if CH_EXP
+  {
+    const unsigned long long te = CH_T();
+    if (lane == 0 && blockIdx.y == 0 && blockIdx.x < 8192 && a.kh == g_ch_sel[0] && a.kw == g_ch_sel[1] &&
+        a.h == g_ch_sel[2] && a.cin == g_ch_sel[3] && a.cout == g_ch_sel[4]) {
+      unsigned long long* o = g_ch_t + (blockIdx.x * 4 + wave) * 8;
+      o[0] = ch_sum[0];
+      o[1] = ch_sum[1];
+      o[2] = ch_sum[2];
+      o[3] = ch_sum[3];
+      o[4] = te - ch_b;
+      o[5] = te - ch_t0;
+      o[6] = (unsigned long long)ch_n;
+      o[7] = ch_t0;
+    }
+  }
+#endif
 }
 
 template <int KH, int KW, int CK, int BN, int TW, int PRO, int EPI, bool POOL, bool V4 = true,
@@ -668,3 +719,13 @@ void conv_h3_split_weights(const float* w, int kh, int kw, int cin, int cout, in
         lo[o] = f32_to_f16_bits(v - (float)h);
       }
 }
+
+#if CH_EXP
+extern "C" int mmla_debug_conv_select(int kh, int kw, int h, int cin, int cout) {
+  const int sel[5] = {kh, kw, h, cin, cout};
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_ch_sel), sel, sizeof(sel));
+}
+extern "C" int mmla_debug_conv_times(unsigned long long* host) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ch_t), sizeof(g_ch_t));
+}
+#endif
