@@ -76,3 +76,68 @@ def sharded_predict(pcm_all, model_kind, ctx, rank, world, on_device=None):
     if on_device:
         t = t.to(f'cuda:{ctx.device}')
     return gather_logits(t, len(pcm_all))
+
+
+# ---- SI whole-conversation mode sharded by frame range ----------------------------
+# speaker_identification_post_processing.py:255-272 computes MFCC + deltas over the WHOLE conversation
+# and predicts its 256-frame windows in one batch.  A rank owns a contiguous range of windows; the
+# frames it needs beyond them are the halo: MFCC(t) reads samples [160 t, 160 t + 400) after a
+# pre-emphasis that needs sample 160 t - 1, and delta-delta(t) reads MFCC(t - 4 .. t + 4).  So the
+# rank computes frames [f0 - 5, f1 + 4) from its own slice of the signal (the 5th frame before f0 only
+# absorbs the slice's pre-emphasis start and the deltas' edge padding) and keeps [f0, f1): identical
+# to the single-process features, with no collective before the logits gather.
+SI_WIN_FRAMES, SI_HOP, SI_FRAME = 256, 160, 400
+_HALO_BEFORE, _HALO_AFTER = 5, 4
+
+
+def conversation_frames(n_samples):
+    """psf framesig's frame count and the number of 256-frame windows of a conversation."""
+    t = 1 if n_samples <= SI_FRAME else 1 + -(-(n_samples - SI_FRAME) // SI_HOP)
+    return t, -(-t // SI_WIN_FRAMES)
+
+
+def conversation_shard(n_samples, rank, world):
+    """-> (w0, w1, s_lo, s_hi, keep): this rank's windows [w0, w1), the signal slice [s_lo, s_hi)
+    it computes features on, and the first kept frame's index within that slice's frames."""
+    t, s = conversation_frames(n_samples)
+    w0, w1 = shard_range(s, rank, world)
+    if w1 <= w0:                        # more ranks than windows: nothing to compute
+        return w0, w1, 0, 0, 0
+    f0, f1 = w0 * SI_WIN_FRAMES, min(w1 * SI_WIN_FRAMES, t)
+    a = max(f0 - _HALO_BEFORE, 0)
+    b = min(f1 + _HALO_AFTER, t)
+    s_hi = n_samples if b == t else SI_HOP * (b - 1) + SI_FRAME
+    return w0, w1, SI_HOP * a, s_hi, f0 - a
+
+
+def conversation_features_shard(sig, rank, world, features_seq):
+    """This rank's windows of the conversation's [S, 256, 39] features (float32, as the kernel
+    returns them).  ``features_seq(slice) -> [S', 256, 39]`` is the whole-signal feature call
+    (``Context.si_features_seq``)."""
+    import numpy as np
+    sig = np.ascontiguousarray(sig, dtype=np.int16).ravel()
+    t, _ = conversation_frames(sig.size)
+    w0, w1, s_lo, s_hi, keep = conversation_shard(sig.size, rank, world)
+    out = np.zeros((w1 - w0, SI_WIN_FRAMES, 39), np.float32)
+    if w1 <= w0:
+        return out
+    f = np.asarray(features_seq(sig[s_lo:s_hi])).reshape(-1, 39)
+    n_keep = min(w1 * SI_WIN_FRAMES, t) - w0 * SI_WIN_FRAMES
+    out.reshape(-1, 39)[:n_keep] = f[keep:keep + n_keep]
+    return out
+
+
+def sharded_conversation_predict(sig, ctx, rank, world, on_device=None):
+    """post_analysing's whole-conversation predict (speaker_identification_post_processing.py:
+    255-272) sharded by window range: this rank's windows through SI-NET on ctx, the logits
+    all-gathered in window order -> [S, K] on every rank."""
+    import numpy as np
+    feat = conversation_features_shard(sig, rank, world, ctx.si_features_seq)
+    probs = ctx.si_forward(feat) if len(feat) else np.zeros((0, ctx.si_classes), np.float32)
+    if on_device is None:
+        on_device = dist.is_initialized() and dist.get_backend() != 'gloo'
+    t = torch.from_numpy(np.ascontiguousarray(probs, dtype=np.float32))
+    if on_device:
+        t = t.to(f'cuda:{ctx.device}')
+    _, s = conversation_frames(np.asarray(sig).size)
+    return gather_logits(t, s)

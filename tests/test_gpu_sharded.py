@@ -41,6 +41,11 @@ def _inputs():
     return synth.batch(4000, N_OD, 40000), synth.batch(4100, N_SI, 24000)
 
 
+def _conversation():
+    """~33 s conversation: 13 windows of 256 frames (7 + 6 per rank), a partial last window"""
+    return np.concatenate([synth.clip(4200 + k, 40960) for k in range(13)])[:13 * 256 * 160 - 5000]
+
+
 def _rank(rank, world, port, out_dir):
     import torch.distributed as dist
     os.environ['MASTER_ADDR'] = '127.0.0.1'
@@ -55,6 +60,12 @@ def _rank(rank, world, port, out_dir):
     p_si = sharded_predict(si, 1, ctx, rank, world, on_device=False)
     np.save(os.path.join(out_dir, f'od_{rank}.npy'), p_od.numpy())
     np.save(os.path.join(out_dir, f'si_{rank}.npy'), p_si.numpy())
+    from mmla_audio_amd.distributed import conversation_features_shard, sharded_conversation_predict
+    conv = _conversation()
+    np.save(os.path.join(out_dir, f'convfeat_{rank}.npy'),
+            conversation_features_shard(conv, rank, world, ctx.si_features_seq))
+    np.save(os.path.join(out_dir, f'conv_{rank}.npy'),
+            sharded_conversation_predict(conv, ctx, rank, world, on_device=False).numpy())
     dist.barrier()
     dist.destroy_process_group()
     ctx.close()
@@ -72,3 +83,12 @@ def test_two_ranks_on_one_gpu_match_single_process(tmp_path):
     for r in range(2):
         assert np.array_equal(np.load(tmp_path / f'od_{r}.npy'), ref_od)
         assert np.array_equal(np.load(tmp_path / f'si_{r}.npy'), ref_si)
+    # SI whole-conversation mode sharded by window range (distributed.sharded_conversation_predict):
+    # each rank's windows from its own slice + halo equal the single-process windows bit for bit
+    conv = _conversation()
+    whole = ctx.si_features_seq(conv)
+    assert np.array_equal(np.concatenate([np.load(tmp_path / f'convfeat_{r}.npy') for r in range(2)]),
+                          whole)
+    ref_conv = ctx.si_forward(whole)
+    for r in range(2):
+        assert np.array_equal(np.load(tmp_path / f'conv_{r}.npy'), ref_conv)
