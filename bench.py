@@ -67,6 +67,7 @@ def parse():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-f32', action='store_true', help='skip the exact-f32 precision leg')
     ap.add_argument('--no-parity', action='store_true', help='skip the oracle parity sample')
+    ap.add_argument('--no-latency', action='store_true', help='skip the batch-1 latency probe')
     ap.add_argument('--microbatch', type=int, default=0,
                     help='clips per internal micro-batch (0 = the library default)')
     ap.add_argument('--cpu-seconds', type=float, default=20.0)
@@ -359,6 +360,22 @@ def main():
         else:
             parity = parity_sample(ctx, wl, pcm, probs, argmax, W, mb, clip_len)
 
+    # batch-1 latency of the host-pointer call the reference's real-time loop makes (one 2.56 s
+    # window per predict, record_on_pc.py:139-160): median of 20 after 5 warmups, outside the
+    # timed region; informational (the headline is the batched throughput above)
+    latency = None
+    if pipeline and world == 1 and not args.no_latency:
+        one = np.ascontiguousarray(pcm[:1].cpu().numpy())
+        call = ctx.od_pipeline if wl == 'od_pipeline' else ctx.si_pipeline
+        ts = []
+        for i in range(25):
+            t0 = time.perf_counter()
+            call(one)
+            if i >= 5:
+                ts.append(time.perf_counter() - t0)
+        latency = {'batch1_ms_median': 1e3 * float(np.median(ts)), 'batch1_ms_p90':
+                   1e3 * float(np.percentile(ts, 90)), 'call': f'{wl} host pointers, 1 clip'}
+
     devices = rank_devices(world, rank, local)
     if rank == 0:
         desc = {
@@ -390,6 +407,7 @@ def main():
             'world_size': world, 'gpus_requested': args.gpus, 'rank_devices': devices,
             'roofline': roof, 'stages': stages, 'fe': fe, 'precision_f32': f32,
             'range_guard_ok': range_ok, 'cpu_baseline': cpu, 'parity': parity,
+            'latency': latency,
         }
         print(json.dumps(line), flush=True)
     if world > 1:
