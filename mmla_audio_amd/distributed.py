@@ -133,6 +133,8 @@ def sharded_conversation_predict(sig, ctx, rank, world, on_device=None):
     all-gathered in window order -> [S, K] on every rank."""
     import numpy as np
     feat = conversation_features_shard(sig, rank, world, ctx.si_features_seq)
+    if ctx.si_classes is None:
+        raise RuntimeError('load the SI weights (Context.load_weights) before predicting')
     probs = ctx.si_forward(feat) if len(feat) else np.zeros((0, ctx.si_classes), np.float32)
     if on_device is None:
         on_device = dist.is_initialized() and dist.get_backend() != 'gloo'
