@@ -13,7 +13,7 @@ grep '^{' gpurun_out/bench_fe.json.log > gpurun_out/bench_fe.json
 timeout -k 10 600 python3 -u bench.py --workload noise_gate > gpurun_out/bench_nr.json.log 2>&1 || exit $?
 grep '^{' gpurun_out/bench_nr.json.log > gpurun_out/bench_nr.json
 rm -rf gpurun_out/prof_bench
-timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_bench -o od -- python3 -u bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-f32 --no-parity > gpurun_out/prof_bench.log 2>&1 || exit $?
+timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_bench -o od -- python3 -u bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-f32 --no-parity --no-latency > gpurun_out/prof_bench.log 2>&1 || exit $?
 python3 - <<'PY'
 import json
 for f in ('od', 'si', 'fe', 'nr'):

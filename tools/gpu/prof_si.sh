@@ -4,7 +4,7 @@ cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 rm -rf gpurun_out/prof_si
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_si -o si -- python3 -u bench.py --workload si_pipeline --steps 2 --warmup 1 --no-cpu-baseline --no-f32 --no-parity > gpurun_out/prof_si.log 2>&1 || exit $?
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_si -o si -- python3 -u bench.py --workload si_pipeline --steps 2 --warmup 1 --no-cpu-baseline --no-f32 --no-parity --no-latency > gpurun_out/prof_si.log 2>&1 || exit $?
 find gpurun_out/prof_si -type f ! -name '*_stats.csv' -delete
 python3 - <<'PY'
 import csv, glob
