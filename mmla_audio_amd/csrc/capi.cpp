@@ -242,6 +242,12 @@ int ws_get(mmla_ctx* c, int slot, size_t bytes, void** out) {
       HIPCHK(c, hipMemsetAsync(p, kGuardByte, guard, c->stream));
       HIPCHK(c, hipMemsetAsync(static_cast<char*>(p) + guard + bytes, kGuardByte, guard, c->stream));
     }
+    // Debug aid: MMLA_WS_POISON=<byte> fills every new slot with that byte (0xff: float NaN), so a
+    // kernel that reads workspace memory no earlier launch wrote shows up in its results
+    const char* pe = std::getenv("MMLA_WS_POISON");
+    if (pe && pe[0])
+      HIPCHK(c, hipMemsetAsync(static_cast<char*>(p) + guard, (int)std::strtol(pe, nullptr, 0) & 255,
+                               bytes, c->stream));
     c->ws[slot] = static_cast<char*>(p) + guard;
     c->ws_size[slot] = bytes;
     c->ws_guard[slot] = guard;

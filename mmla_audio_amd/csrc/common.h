@@ -44,6 +44,15 @@ MMLA_DEV T wave_sum(T v) {
   return v;
 }
 
+// A wave that re-reads global memory it stored itself in the same launch must wait for its own
+// stores first.  __threadfence_block() does NOT do that on gfx950 (workgroup scope on one CU lowers
+// to no vmcnt wait), so a load issued behind it can overtake the store and return the OLD bytes --
+// seen only under load: kernels co-running on the CU delayed the stores of the front-ends' scratch /
+// cepstra rows, and the re-read took the previous micro-batch's values (tests/test_gpu_corun.py).
+// vmcnt(0) returns once every store of the wave is acknowledged by L2; the re-reading loads then
+// miss this CU's L1 (no earlier load of these lines in this launch) and read L2.
+MMLA_DEV void wave_stores_done() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
 // Kernel launch wrappers are declared extern "C++" here and defined in the .hip files; the C ABI
 // (capi.cpp) calls them.
 struct OdFeTables;  // device constant tables for the OD front-end

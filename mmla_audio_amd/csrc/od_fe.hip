@@ -455,7 +455,7 @@ __global__ void __launch_bounds__(NT, 2) od_fe_kernel(OdFeArgs a) {
   // ---- clip max / min of the mel power (one wave: shuffles only) ----------------------------------
   smax = wave_max(smax);
   smin = wave_min(smin);
-  __threadfence_block();   // the scratch stores have completed: visible to this CU's re-reads
+  wave_stores_done();   // this wave's scratch stores have completed (common.h)
   lds_order();
 
   // power_to_db(ref=np.max, amin=1e-10, top_db=80) with numpy-1.21 dtypes, then normalize_matrix.

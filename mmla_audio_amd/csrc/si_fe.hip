@@ -375,7 +375,7 @@ __global__ void __launch_bounds__(NT, 2) si_fe_kernel(SiFeArgs a) {
 #undef SI_PREFETCH
 
   // ---- epilogue: cepstra of local frames [g_lo, g_hi) into LDS, then the 39 output columns --------
-  __threadfence_block();   // this wave's cepstra stores have completed
+  wave_stores_done();   // this wave's cepstra stores have completed (common.h)
   lds_order();
   float* C = reinterpret_cast<float*>(&sm.z[0][0]);   // [NL][13]
   constexpr int CPL = (NL * 13 + NT - 1) / NT;         // 54
