@@ -242,6 +242,9 @@ int mmla_profile_enable(mmla_ctx* ctx, int on);
  * 11 = BiLSTM output [n,512]) and copy that tensor to host `out` (capacity out_floats). */
 int mmla_debug_od_trace(mmla_ctx* ctx, const float* x, int64_t n, int stage, float* out,
                         int64_t out_floats);
+/* Debug (tests, tools): device address and size of internal workspace slot `slot` (0 and 0 when the
+ * slot was never allocated), e.g. to check that no kernel of another call writes into it. */
+int mmla_debug_ws_slot(mmla_ctx* ctx, int slot, void** ptr, size_t* bytes);
 /* ms[MMLA_NSTAGES], launches[MMLA_NSTAGES], work[MMLA_NSTAGES] (each nullable); reset != 0 clears */
 int mmla_profile_read(mmla_ctx* ctx, double* ms, int64_t* launches, double* work, int reset);
 

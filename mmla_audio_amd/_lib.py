@@ -57,6 +57,7 @@ SIGNATURES = {
     'mmla_profile_enable': [_P, ctypes.c_int],
     'mmla_profile_read': [_P, _P, _P, _P, ctypes.c_int],
     'mmla_debug_od_trace': [_P, _P, _I64, ctypes.c_int, _P, _I64],
+    'mmla_debug_ws_slot': [_P, ctypes.c_int, _P, _P],
     'mmla_vad_reset': [_P, _I64, _I32],
     'mmla_vad_remove_silence': [_P, _P, _I64, _I64, _P, _I32, _I64, _P, _P, _P, _I32, _U32],
     'mmla_vad_collect': [_P, _P, _I64, _I64, _P, _I32, _P, _I32, _P, _P, _U32],

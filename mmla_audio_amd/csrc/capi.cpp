@@ -1626,6 +1626,14 @@ int mmla_debug_od_trace(mmla_ctx* c, const float* x, int64_t n, int stage, float
   return MMLA_OK;
 }
 
+int mmla_debug_ws_slot(mmla_ctx* c, int slot, void** ptr, size_t* bytes) {
+  if (!c || !ptr || !bytes || slot < 0) return MMLA_E_INVALID;
+  const bool have = slot < (int)c->ws.size() && c->ws[slot];
+  *ptr = have ? c->ws[slot] : nullptr;
+  *bytes = have ? c->ws_size[slot] : 0;
+  return MMLA_OK;
+}
+
 int mmla_profile_enable(mmla_ctx* c, int on) {
   if (!c) return MMLA_E_INVALID;
   c->prof_on = on != 0;

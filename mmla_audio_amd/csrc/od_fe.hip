@@ -154,8 +154,19 @@ MMLA_DEV void dft10(cf v[10]) {
 MMLA_DEV float db10(float s) { return __log2f(fmaxf(1e-10f, s)) * 3.0102999566398120f; }
 
 // wave-local LDS ordering: a wave's DS operations execute in issue order, so lanes of ONE wave
-// only need the compiler not to move LDS accesses across this point (no s_barrier, no vmcnt wait)
-MMLA_DEV void lds_order() { asm volatile("" ::: "memory"); }
+// only need the compiler not to move LDS accesses across this point (no s_barrier, no lgkmcnt wait).
+// (FE_LDS_WAIT=1 turns it into an lgkmcnt(0) wait: used in round 2 to rule LDS ordering out as the
+// cause of the co-run corruption that packed-FP32 instructions turned out to cause, common.h.)
+#ifndef FE_LDS_WAIT
+#define FE_LDS_WAIT 0
+#endif
+MMLA_DEV void lds_order() {
+#if FE_LDS_WAIT
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#else
+  asm volatile("" ::: "memory");
+#endif
+}
 
 // ================================================================================================
 namespace v2 {
@@ -190,7 +201,10 @@ MMLA_DEV void split_power(cf z, cf zr, cf w, float& pk, float& pnk) {
 // DB / NM / IMG: which of the dB, normalised and image outputs are written (compile-time, so the
 // epilogue's store counts are static and its waits for the scratch re-reads stay counted)
 template <bool DB, bool NM, bool IMG>
-__global__ void __launch_bounds__(NT, 2) od_fe_kernel(OdFeArgs a) {
+#ifndef FE_MINB
+#define FE_MINB 2   // waves (= workgroups) per SIMD the register budget is sized for
+#endif
+__global__ void MMLA_NO_PK_F32 __launch_bounds__(NT, FE_MINB) od_fe_kernel(OdFeArgs a) {
   __shared__ __attribute__((aligned(16))) Smem sm;
   const OdFeTables& tb = *a.tables;
   const int lane = threadIdx.x;

@@ -21,8 +21,12 @@
 // K runs over (tap, channel) with the channel fastest, so CIN = 16 packs two taps per k-step.
 // 3xFP16 as in conv_h3.hip: activations x 2^4 and weights x 2^8 split into hi + lo (lo unscaled),
 // ONE accumulator per tile: acc += hi*hi + hi*lo + lo*hi; value = acc * 2^-12.
+#include "common.h"
 #include "resblk.h"
 
+#ifndef RB_W2LDS
+#define RB_W2LDS 1   // GEMM 2's weights staged in LDS (0: read from L2)
+#endif
 #ifndef RB_EXP
 #define RB_EXP 0   // experiment switch for profiling (0 = product)
 #endif
@@ -129,7 +133,7 @@ struct Geo {
   static constexpr int LW2 = 4 * C + 16;           // halfs per LDS row of GEMM 2's weights (288 B)
   // GEMM 2's weights live in LDS (B from L2 in GEMM 2 cost more than a third workgroup per CU
   // bought for the 16-channel block: measured)
-  static constexpr bool W2LDS = true;
+  static constexpr bool W2LDS = RB_W2LDS;
   static constexpr int W2 = W2LDS ? C * LW2 : 0;
   static constexpr int MINB = 2;                   // resident workgroups per CU (LDS budget)
   static constexpr int PF = 3;                     // GEMM 1 B fragments in flight (k-steps)
@@ -142,7 +146,7 @@ struct Geo {
 
 // STEM: the block input is the stem Conv2D(16, 1x1) of the image, computed while staging (block 1)
 template <int CIN, int C, bool POOL, bool STEM>
-__global__ void __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(ResBlkArgs a) {
+__global__ void MMLA_NET_ATTR __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(ResBlkArgs a) {
   using G = Geo<CIN, C, POOL>;
   constexpr int XC = G::XC, XPS = G::XPS, TPS = G::TPS, MT1 = G::MT1, MT2 = G::MT2, NTW = G::NTW;
   constexpr int KS1 = G::KS1, K1PAD = G::K1PAD, KS2 = G::KS2, PF = G::PF, QPP = G::QPP;

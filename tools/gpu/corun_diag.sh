@@ -1,9 +1,14 @@
 #!/bin/bash
-# dev: co-run matrix after the front-end store-wait fix, then the full GPU suite
+# dev: FE corruption next to resblk: register-capped FE with packed FP32 (minb3); FE throughput of
+# the product build, the no-packed-FP32 build and the capped build
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 300 python3 -u tools/corun_diag4.py > gpurun_out/corun4.log 2>&1 || { tail -20 gpurun_out/corun4.log; exit 1; }
-grep -v amdgpu.ids gpurun_out/corun4.log
-timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/suite.log 2>&1
-rc=$?; tail -3 gpurun_out/suite.log; [ $rc -eq 0 ] || { grep -E "Error|assert" gpurun_out/suite.log | head; exit $rc; }
+MMLA_LIB=mmla_audio_amd/ab/libmmla_minb3.so timeout -k 10 300 python3 -u tools/corun_diag7.py > gpurun_out/corun7d.log 2>&1 || { tail -20 gpurun_out/corun7d.log; exit 1; }
+grep -v amdgpu.ids gpurun_out/corun7d.log
+for lib in mmla_audio_amd/libmmla.so mmla_audio_amd/ab/libmmla_nopk.so mmla_audio_amd/ab/libmmla_minb3.so; do
+  for n in 4096 65536; do
+    timeout -k 10 300 python3 tools/bench_with_lib.py $lib --workload od_features --clips $n --steps 5 --warmup 2 --no-cpu-baseline > gpurun_out/fe_ab.log 2>&1 || exit $?
+    python3 -c "import json;d=json.loads([l for l in open('gpurun_out/fe_ab.log') if l.startswith('{')][0]);r=d['roofline'];print('$lib',$n,'clips/s',round(d['value']),'frac',round(r['frac'],4))"
+  done
+done
