@@ -44,23 +44,6 @@ MMLA_DEV T wave_sum(T v) {
   return v;
 }
 
-// Kernels that must not use packed-FP32 VALU instructions (v_pk_fma/mul/add_f32).  Measured on
-// MI355X (ROCm 7.2): a one-wave-per-workgroup front-end wave using them returned wrong values in one
-// 16-lane quarter of an instruction, a few times per thousand waves, while workgroups of an MFMA
-// kernel (resblk.hip) of another stream ran on the same CU; built without them the same co-run is
-// bit-exact, and the front-end is also faster (fewer register-pair moves).  See DESIGN.md section 4.
-#ifdef __HIP_DEVICE_COMPILE__   // (a device-code target feature: the host pass has none to drop)
-#define MMLA_NO_PK_F32 __attribute__((target("no-packed-fp32-ops")))
-#else
-#define MMLA_NO_PK_F32
-#endif
-// the network kernels (resblk, conv_h3, bilstm_h3) with MMLA_NETS_NO_PK=1 (dev A/B)
-#if defined(MMLA_NETS_NO_PK) && MMLA_NETS_NO_PK
-#define MMLA_NET_ATTR MMLA_NO_PK_F32
-#else
-#define MMLA_NET_ATTR
-#endif
-
 // A wave that re-reads global memory it stored itself in the same launch must wait for its own
 // stores first.  __threadfence_block() does NOT do that on gfx950 (workgroup scope on one CU lowers
 // to no vmcnt wait), so a load issued behind it can overtake the store and return the OLD bytes --

@@ -108,7 +108,7 @@ template <class S> MMLA_DEV constexpr int shp_co() { return ShapeOf<S>::co; }
 
 template <int KH, int KW, int CK, int BN, int TW, int PRO, int EPI, bool POOL, bool V4 = true,
           bool PIN = false, class SHP = Shape<0, 0, 0, 0>>
-__global__ void MMLA_NET_ATTR __launch_bounds__(NT, 2) conv_h3_kernel(ConvH3Args a) {
+__global__ void __launch_bounds__(NT, 2) conv_h3_kernel(ConvH3Args a) {
   // each wave owns ONE 32-column slice of B (no B fragment is loaded by two waves) and
   // 128 / WM rows: BN 32 -> 4 x 1, BN 64 -> 2 x 2, BN 128 -> 1 x 4 (waves along N)
   constexpr int WN = BN / 32;

@@ -203,7 +203,7 @@ MMLA_DEV void split1(float v, _Float16& h, _Float16& l) {   // v * 2^6 = hi + lo
 // MT 32-clip row tiles per workgroup (1, or 2 where the batch still fills the chip: half the weight
 // stream per clip); PF: prefetch the next k-step's B fragments (MT 1 only: registers)
 template <int D, int MT>
-__global__ void MMLA_NET_ATTR __launch_bounds__(512) bilstm_h3_kernel(const float* __restrict__ seq, int n, int T,
+__global__ void __launch_bounds__(512) bilstm_h3_kernel(const float* __restrict__ seq, int n, int T,
                                                         const uint16_t* __restrict__ wfh,
                                                         const uint16_t* __restrict__ wfl,
                                                         const uint16_t* __restrict__ wbh,

@@ -24,6 +24,13 @@
 // clip's normalisation needs the clip-global max/min, so the dB rows go to a frame-major HBM
 // scratch that the epilogue re-reads (8-band column blocks, transposed through LDS).
 //
+// Built WITHOUT packed-FP32 instructions (v_pk_fma/mul/add_f32; Makefile NO_PK_F32): on MI355X a
+// front-end wave using them returned wrong values in one 16-lane quarter of an instruction, a few
+// times per thousand waves, while MFMA workgroups of another stream (resblk.hip) shared the CUs;
+// without them the same co-run is bit-exact and the kernel is 7-12 % faster.
+// (A per-kernel target attribute is not enough: the HIP headers' helpers, e.g. float2's constructor
+// and threadIdx, then stop inlining across the feature mismatch and spill to scratch.)
+//
 // Arithmetic is float32 (the reference runs the FFT in float64 and stores complex64; the measured
 // deviation on the normalised log-mel is ~1e-5, tolerance 1e-4).  The scalar steps
 // that the reference does in float64 (ref dB, image quantisation) are done in float64 here.
@@ -204,7 +211,7 @@ template <bool DB, bool NM, bool IMG>
 #ifndef FE_MINB
 #define FE_MINB 2   // waves (= workgroups) per SIMD the register budget is sized for
 #endif
-__global__ void MMLA_NO_PK_F32 __launch_bounds__(NT, FE_MINB) od_fe_kernel(OdFeArgs a) {
+__global__ void __launch_bounds__(NT, FE_MINB) od_fe_kernel(OdFeArgs a) {
   __shared__ __attribute__((aligned(16))) Smem sm;
   const OdFeTables& tb = *a.tables;
   const int lane = threadIdx.x;

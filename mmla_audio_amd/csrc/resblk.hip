@@ -21,7 +21,6 @@
 // K runs over (tap, channel) with the channel fastest, so CIN = 16 packs two taps per k-step.
 // 3xFP16 as in conv_h3.hip: activations x 2^4 and weights x 2^8 split into hi + lo (lo unscaled),
 // ONE accumulator per tile: acc += hi*hi + hi*lo + lo*hi; value = acc * 2^-12.
-#include "common.h"
 #include "resblk.h"
 
 #ifndef RB_W2LDS
@@ -146,7 +145,7 @@ struct Geo {
 
 // STEM: the block input is the stem Conv2D(16, 1x1) of the image, computed while staging (block 1)
 template <int CIN, int C, bool POOL, bool STEM>
-__global__ void MMLA_NET_ATTR __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(ResBlkArgs a) {
+__global__ void __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(ResBlkArgs a) {
   using G = Geo<CIN, C, POOL>;
   constexpr int XC = G::XC, XPS = G::XPS, TPS = G::TPS, MT1 = G::MT1, MT2 = G::MT2, NTW = G::NTW;
   constexpr int KS1 = G::KS1, K1PAD = G::K1PAD, KS2 = G::KS2, PF = G::PF, QPP = G::QPP;
