@@ -93,14 +93,6 @@ __device__ __forceinline__ float4 image_px(const ResBlkArgs& a, int64_t pix) {
   const float* p = a.imgf + pix * 3;
   return make_float4(p[0], p[1], p[2], 0.f);
 }
-// Conv2D(16, 1x1) stem channel co of one pixel, in the stem kernel's order (nets.hip od_stem_kernel)
-__device__ __forceinline__ float stem_ch(const ResBlkArgs& a, float4 x, int co) {
-  float acc = x.x * a.wst[0 * a.ldst + co];
-  acc = fmaf(x.y, a.wst[1 * a.ldst + co], acc);
-  acc = fmaf(x.z, a.wst[2 * a.ldst + co], acc);
-  return acc + a.bst[co];
-}
-
 template <int CIN, int C, bool POOL>
 struct Geo {
   static constexpr int WN = 1;                     // waves along N: each wave owns all C columns,
@@ -173,14 +165,38 @@ __global__ void __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(R
   const int q = tid % QPP;
   const float4 sc4 = *reinterpret_cast<const float4*>(a.s1 + 4 * q);
   const float4 sh4 = *reinterpret_cast<const float4*>(a.t1 + 4 * q);
-  float stw[3][4], stb[4];   // STEM: this thread's stem weights (channels 4q .. 4q+3)
+  // STEM: the image halo is loaded ONCE per pixel (not once per channel quad) into LDS as float4
+  // {r, g, b, inside-image}, the stem weights as [co] float4 {w_r, w_g, w_b, bias}; the staging and
+  // the shortcut operands read both from LDS behind one extra barrier.  Both live past the halo's
+  // hi/lo planes, inside bytes that t1 only takes after GEMM 1 (GEMM 1's padded rows may read them:
+  // finite fp16 patterns).  Per thread this issues <= 7 loads where the per-task image and per-channel
+  // weight loads were ~50 (RB_EXP timeline: the halo phase was the longest of block 1).
+  float4* const s_img = reinterpret_cast<float4*>(smem + G::XREG);
+  float4* const s_wst = s_img + G::XNP;
+  static_assert(!STEM || (G::XREG % 8 == 0 && G::XREG * 2 + (G::XNP + 16) * 16 <= G::SM * 2),
+                "stem staging buffers fit behind the halo planes");
+  float stw[3][4], stb[4];   // STEM: this thread's stem weights (channels 4q .. 4q+3), from s_wst
   if constexpr (STEM) {
+    constexpr int PPT = (G::XNP + NT - 1) / NT;   // pixels per thread
+    float4 im[PPT];
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-#pragma unroll
-      for (int k = 0; k < 3; ++k) stw[k][c] = a.wst[k * a.ldst + 4 * q + c];
-      stb[c] = a.bst[4 * q + c];
+    for (int k = 0; k < PPT; ++k) {
+      const int p = tid + k * NT;
+      im[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+      const int py = p / XC, pxx = p - (p / XC) * XC;
+      const int ih = h0 - 2 + py, iw = w0 - 1 + pxx;
+      if (p < G::XNP && ih >= 0 && ih < a.h && iw >= 0 && iw < a.w) {
+        im[k] = image_px(a, ((int64_t)clip * a.h + ih) * a.w + iw);
+        im[k].w = 1.0f;
+      }
     }
+    if (tid < 64) {   // [co][k]: k < 3 weights of the r, g, b inputs, k = 3 the bias
+      const int co = tid >> 2, k = tid & 3;
+      reinterpret_cast<float*>(s_wst)[tid] = k < 3 ? a.wst[k * a.ldst + co] : a.bst[co];
+    }
+#pragma unroll
+    for (int k = 0; k < PPT; ++k)
+      if (tid + k * NT < G::XNP) s_img[tid + k * NT] = im[k];
   }
   float ps2[NTW], pb1[NTW], pt2[NTW], pbo[NTW];   // BN2 scale / conv-1 bias / BN2 shift, out bias
 #pragma unroll
@@ -208,9 +224,7 @@ __global__ void __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(R
 #if RB_EXP == 1
           pre[j] = make_float4(0.01f * ih, 0.02f * iw, 0.f, 1.f);
 #else
-          if constexpr (STEM) {
-            pre[j] = image_px(a, ((int64_t)clip * a.h + ih) * a.w + iw);
-          } else {
+          if constexpr (!STEM) {   // (STEM: from s_img after the barrier below)
             pre[j] = *reinterpret_cast<const float4*>(xc + (ih * a.w + iw) * CIN);
           }
 #endif
@@ -245,18 +259,10 @@ __global__ void __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(R
       for (int j = 0; j < MSC; ++j) {
         const int ih = h0 + 2 * (wm * (MT2 / 2) + 2 * j + pr), iw = w0 + 2 * pc;
         scx[s][j][0] = scx[s][j][1] = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (ci < CIN && ih < a.h && iw < a.w) {
-          if constexpr (STEM) {
-            const float4 x = image_px(a, ((int64_t)clip * a.h + ih) * a.w + iw);
-            scx[s][j][0] = make_float4(stem_ch(a, x, ci), stem_ch(a, x, ci + 1), stem_ch(a, x, ci + 2),
-                                       stem_ch(a, x, ci + 3));
-            scx[s][j][1] = make_float4(stem_ch(a, x, ci + 4), stem_ch(a, x, ci + 5),
-                                       stem_ch(a, x, ci + 6), stem_ch(a, x, ci + 7));
-          } else {
-            const float* src = xc + (ih * a.w + iw) * CIN + ci;
-            scx[s][j][0] = *reinterpret_cast<const float4*>(src);
-            scx[s][j][1] = *reinterpret_cast<const float4*>(src + 4);
-          }
+        if (!STEM && ci < CIN && ih < a.h && iw < a.w) {   // (STEM: from LDS after the barrier)
+          const float* src = xc + (ih * a.w + iw) * CIN + ci;
+          scx[s][j][0] = *reinterpret_cast<const float4*>(src);
+          scx[s][j][1] = *reinterpret_cast<const float4*>(src + 4);
         }
       }
     }
@@ -282,6 +288,49 @@ __global__ void __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(R
       bh[s][nt] = *reinterpret_cast<const f16x8*>(a.w1h + b1o + nt * 16 * K1PAD + 32 * s);
       bl[s][nt] = *reinterpret_cast<const f16x8*>(a.w1l + b1o + nt * 16 * K1PAD + 32 * s);
     }
+
+  if constexpr (STEM) {
+    __syncthreads();   // s_img / s_wst staged
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const float4 wv = s_wst[4 * q + c];
+      stw[0][c] = wv.x;
+      stw[1][c] = wv.y;
+      stw[2][c] = wv.z;
+      stb[c] = wv.w;
+    }
+#pragma unroll
+    for (int j = 0; j < MAXT; ++j) {
+      const int px = (tid + j * NT) / QPP;
+      if (px < G::XNP) pre[j] = s_img[px];   // .w = 1 inside the image, matching `valid`
+    }
+    if constexpr (POOL) {   // the shortcut's raw stem channels ci .. ci + 7 of its pixel
+      const int p = col;
+      const int pr = (p & 3) >> 1, pc = 2 * (p >> 2) + (p & 1);
+#pragma unroll
+      for (int s = 0; s < KSC; ++s) {
+        const int ci = 32 * s + 8 * grp;
+#pragma unroll
+        for (int j = 0; j < MSC; ++j) {
+          // tile pixel (2 (wm MT2/2 + 2j + pr), 2 pc) = halo pixel (+2 rows, +1 column)
+          const float4 x = s_img[(2 * (wm * (MT2 / 2) + 2 * j + pr) + 2) * XC + 2 * pc + 1];
+          if (ci < CIN && x.w != 0.0f) {
+            float o[8];
+#pragma unroll
+            for (int c = 0; c < 8; ++c) {   // od_stem_kernel's order
+              const float4 wv = s_wst[ci + c];
+              float acc = x.x * wv.x;
+              acc = fmaf(x.y, wv.y, acc);
+              acc = fmaf(x.z, wv.z, acc);
+              o[c] = acc + wv.w;
+            }
+            scx[s][j][0] = make_float4(o[0], o[1], o[2], o[3]);
+            scx[s][j][1] = make_float4(o[4], o[5], o[6], o[7]);
+          }
+        }
+      }
+    }
+  }
 
   RB_MARK(1);
   // ---- stage: BN1 + ELU once per element, split hi/lo; zero outside the image (conv padding) ----
