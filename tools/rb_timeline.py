@@ -1,12 +1,16 @@
 """Phase timeline of the fused res_block kernel (dev tool): needs a library built with
 -DRB_EXP=4 (s_memtime marks of the first 8192 workgroups of the pool-block launch)."""
 import ctypes
+import os
 import sys
 
 import numpy as np
 
 sys.path.insert(0, '.')
 from mmla_audio_amd import _lib, weights  # noqa: E402
+
+LIB = os.environ.get('MMLA_LIB', _lib.LIB_PATH)   # a -DRB_EXP=4 build
+_lib.load_library(LIB)
 
 ctx = _lib.Context(0)
 W = weights.synthetic(weights.OD, seed=0)
@@ -17,7 +21,7 @@ img = rng.integers(0, 256, size=(n, 128, 151, 3), dtype=np.uint8)
 ctx.od_forward(img)
 ctx.od_forward(img)
 buf = (ctypes.c_ulonglong * (8192 * 4 * 8))()
-lib = ctypes.CDLL(_lib.LIB_PATH)
+lib = ctypes.CDLL(LIB)
 rc = lib.mmla_debug_resblk_times(buf)
 t = np.frombuffer(buf, dtype=np.uint64).reshape(8192, 4, 8).astype(np.int64)
 t0 = t[:, :, 0].min()
