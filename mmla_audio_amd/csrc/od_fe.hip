@@ -184,14 +184,18 @@ constexpr int WIN = (R - 1) * HOP + N_FFT;        // 1200 samples behind one rou
 constexpr int T_LO = 2, T_HI = 9;                 // mel taps of bands 0..63 / 64..127 (host-checked)
 
 constexpr int P2W = 212;           // power-row pitch (>= 201 + the widest band's taps: zero pad)
-struct Smem {                      // 18.0 KB
+// 12.5 KB: three clip-waves per SIMD (12 per CU).  The power spectra of frame pair q live in the
+// pair's own FFT rows: p2(q)[k].c = P[2q + c][k] over the first 1696 B of st[2q], st[2q + 1] (the
+// split reads both frames' Z before it writes the pair's row)
+struct Smem {
   int16_t win[WIN];                // reflect-padded window of the round, base = 160 f0 - 200
-  cf st[R][200];                   // per frame: pass A out [k1][n2] -> Z[k]
-  float2 p2[R / 2][P2W];           // power spectra of frame pairs, interleaved: P[2q + c][k] = p2[q][k].c
+  cf st[R][200];                   // per frame: pass A out [k1][n2] -> Z[k] -> power rows
   int zc[NF + 1];                  // ZCR counts of the clip
   uint8_t rb[NF + 1];              // image R byte per column
 };
 static_assert(sizeof(int16_t) * WIN % 16 == 0, "st must stay 16-B aligned");
+static_assert(P2W * sizeof(float2) <= 2 * 200 * sizeof(cf), "a pair's power row fits its FFT rows");
+MMLA_DEV float2* p2row(Smem& sm, int q) { return reinterpret_cast<float2*>(sm.st[2 * q]); }
 
 // |X[k]|^2 and |X[200 - k]|^2 of the 400-point real DFT from Z[k], Z[200 - k] of the packed FFT
 MMLA_DEV void split_power(cf z, cf zr, cf w, float& pk, float& pnk) {
@@ -209,7 +213,7 @@ MMLA_DEV void split_power(cf z, cf zr, cf w, float& pk, float& pnk) {
 // epilogue's store counts are static and its waits for the scratch re-reads stay counted)
 template <bool DB, bool NM, bool IMG>
 #ifndef FE_MINB
-#define FE_MINB 2   // waves (= workgroups) per SIMD the register budget is sized for
+#define FE_MINB 3   // waves (= workgroups) per SIMD the register budget is sized for (12.5 KB LDS: 12 per CU)
 #endif
 __global__ void __launch_bounds__(NT, FE_MINB) od_fe_kernel(OdFeArgs a) {
   __shared__ __attribute__((aligned(16))) Smem sm;
@@ -267,18 +271,18 @@ __global__ void __launch_bounds__(NT, FE_MINB) od_fe_kernel(OdFeArgs a) {
   // constants kept in registers (LDS reads every frame / round otherwise)
   const cf wka = {tb.w400k[lane][0], tb.w400k[lane][1]};
   const cf wkb = lane + 64 <= 100 ? cf{tb.w400k[lane + 64][0], tb.w400k[lane + 64][1]} : cf{0.f, 0.f};
-  cf hw[20], tw[20];   // pass A: window taps of the lane's n2 and its twiddles W200^(n2 k1)
+  // pass A: window taps of the lane's n2; pass B: twiddles W200^(n2 k1) of the lane's k1 (applied
+  // when pass B reads the row: 9 per lane instead of pass A's 19 -- the registers that let three
+  // waves share a SIMD)
+  cf hw[20], tk[10];
   {
     const int n2 = lane < R * 10 ? lane % 10 : 0;
 #pragma unroll
-    for (int n1 = 0; n1 < 20; ++n1) {
-      hw[n1] = cf{tb.hann2[10 * n1 + n2][0], tb.hann2[10 * n1 + n2][1]};
-      tw[n1] = cf{tb.tw[n1][n2][0], tb.tw[n1][n2][1]};
-    }
+    for (int n1 = 0; n1 < 20; ++n1) hw[n1] = cf{tb.hann2[10 * n1 + n2][0], tb.hann2[10 * n1 + n2][1]};
+    const int k1 = lane < 60 ? lane % 20 : 0;
+#pragma unroll
+    for (int j = 1; j < 10; ++j) tk[j] = cf{tb.tw[k1][j][0], tb.tw[k1][j][1]};
   }
-
-  for (int i = lane; i < (R / 2) * (P2W - 201); i += NT)   // power-row pads read by the last taps
-    sm.p2[i / (P2W - 201)][201 + i % (P2W - 201)] = float2{0.0f, 0.0f};
   static_assert(R % 2 == 0, "frame pairs");
 
   float smax = 0.0f, smin = INFINITY;
@@ -363,8 +367,8 @@ __global__ void __launch_bounds__(NT, FE_MINB) od_fe_kernel(OdFeArgs a) {
       if (lane < R && f0 + lane < NF) sm.zc[f0 + lane] = c - fz;
     }
     FE_MARK(1);
-    // ---- pass A: DFT-20 over n1 of z[10 n1 + n2] (z[m] = hann-windowed (x[2m], x[2m+1])),
-    //      times W200^(n2 k1) -> st[f][k1][n2] ---------------------------------------------------------
+    // ---- pass A: DFT-20 over n1 of z[10 n1 + n2] (z[m] = hann-windowed (x[2m], x[2m+1]))
+    //      -> st[f][k1][n2] (the twiddle W200^(n2 k1) is applied by pass B) ---------------------------
     if (lane < R * 10) {
       const int f = lane / 10, n2 = lane - 10 * f;
       const uint32_t* wp = reinterpret_cast<const uint32_t*>(sm.win) + 80 * f + n2;
@@ -377,13 +381,12 @@ __global__ void __launch_bounds__(NT, FE_MINB) od_fe_kernel(OdFeArgs a) {
       }
       dft20(u);
       cf* dst = &sm.st[f][n2];
-      dst[0] = u[0];
 #pragma unroll
-      for (int k1 = 1; k1 < 20; ++k1) dst[10 * k1] = cmul(u[k1], tw[k1]);
+      for (int k1 = 0; k1 < 20; ++k1) dst[10 * k1] = u[k1];
     }
     lds_order();
     FE_MARK(2);
-    // ---- pass B: DFT-10 over n2 of row st[f][k1][*] -> Z[k1 + 20 k2], in place per frame
+    // ---- pass B: twiddle, then DFT-10 over n2 of row st[f][k1][*] -> Z[k1 + 20 k2], in place per frame
     //      (frames 0-2, then 3-5: a round never reads a frame the other one writes; all of a
     //      round's reads are issued before its writes) -------------------------------------------------
 #pragma unroll
@@ -399,6 +402,8 @@ __global__ void __launch_bounds__(NT, FE_MINB) od_fe_kernel(OdFeArgs a) {
           v[2 * j + 1] = {q.z, q.w};
         }
         lds_order();
+#pragma unroll
+        for (int j = 1; j < 10; ++j) v[j] = cmul(v[j], tk[j]);
         dft10(v);
 #pragma unroll
         for (int k2 = 0; k2 < 10; ++k2) sm.st[f][k1 + 20 * k2] = v[k2];
@@ -406,30 +411,38 @@ __global__ void __launch_bounds__(NT, FE_MINB) od_fe_kernel(OdFeArgs a) {
       lds_order();
     }
     FE_MARK(3);
-    // ---- split: power spectrum P[f][0..200] into the frame pair's interleaved row -----------------
+    // ---- split: power spectra P[f][0..200] of frame pair q into the pair's interleaved row, which
+    //      overlays the pair's Z rows: both frames' Z are read before the first write -------------------
 #pragma unroll
-    for (int f = 0; f < R; ++f) {
-      const cf* Z = sm.st[f];
-      float* P = reinterpret_cast<float*>(sm.p2[f >> 1]) + (f & 1);   // P[k] at P[2 k]
+    for (int q = 0; q < R / 2; ++q) {
       const int ka = lane, kb = lane + 64;
       const bool hb = kb <= 100;
-      const cf za = Z[ka], zar = Z[ka == 0 ? 0 : 200 - ka], wa = wka;
-      cf zb = {0.f, 0.f}, zbr = {0.f, 0.f};
-      const cf wb = wkb;
-      if (hb) {
-        zb = Z[kb];
-        zbr = Z[200 - kb];
+      cf za[2], zar[2], zb[2] = {{0.f, 0.f}, {0.f, 0.f}}, zbr[2] = {{0.f, 0.f}, {0.f, 0.f}};
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const cf* Z = sm.st[2 * q + c];
+        za[c] = Z[ka];
+        zar[c] = Z[ka == 0 ? 0 : 200 - ka];
+        if (hb) {
+          zb[c] = Z[kb];
+          zbr[c] = Z[200 - kb];
+        }
       }
       lds_order();
-      float p0, p1;
-      split_power(za, zar, wa, p0, p1);
-      P[2 * ka] = p0;
-      P[2 * (200 - ka)] = p1;
-      if (hb) {
-        split_power(zb, zbr, wb, p0, p1);
-        P[2 * kb] = p0;
-        P[2 * (200 - kb)] = p1;
+      float* P = reinterpret_cast<float*>(p2row(sm, q));   // P[2q + c][k] at P[2 k + c]
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        float p0, p1;
+        split_power(za[c], zar[c], wka, p0, p1);
+        P[2 * ka + c] = p0;
+        P[2 * (200 - ka) + c] = p1;
+        if (hb) {
+          split_power(zb[c], zbr[c], wkb, p0, p1);
+          P[2 * kb + c] = p0;
+          P[2 * (200 - kb) + c] = p1;
+        }
       }
+      if (lane < 2 * (P2W - 201)) P[2 * 201 + lane] = 0.0f;   // the row pad read by the last taps
     }
     lds_order();
     FE_MARK(4);
@@ -441,7 +454,7 @@ __global__ void __launch_bounds__(NT, FE_MINB) od_fe_kernel(OdFeArgs a) {
     float s0 = 0.0f, s1 = 0.0f;
 #pragma unroll
     for (int q = 0; q < R / 2; ++q) {
-      const float2* P = sm.p2[q];
+      const float2* P = p2row(sm, q);
       float2 a0 = {0.0f, 0.0f}, a1 = {0.0f, 0.0f};
 #pragma unroll
       for (int j = 0; j < T_LO; ++j) {
