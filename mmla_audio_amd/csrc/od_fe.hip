@@ -54,7 +54,7 @@ __device__ unsigned long long g_fe_t[4096 * 8];
     tlast = tn;                                                      \
   } while (0)
 #define FE_T_STORE                                                   \
-  if (lane == 0 && clip < 4096)                                      \
+  if (threadIdx.x == 0 && clip < 4096)                                      \
     for (int i_ = 0; i_ < 8; ++i_) g_fe_t[clip * 8 + i_] = tacc[i_];
 #else
 #define FE_T_INIT
@@ -187,15 +187,30 @@ constexpr int P2W = 212;           // power-row pitch (>= 201 + the widest band'
 // 12.5 KB: three clip-waves per SIMD (12 per CU).  The power spectra of frame pair q live in the
 // pair's own FFT rows: p2(q)[k].c = P[2q + c][k] over the first 1696 B of st[2q], st[2q + 1] (the
 // split reads both frames' Z before it writes the pair's row)
-struct Smem {
+//
+// A clip is FE_NW waves (one workgroup): wave w runs rounds w, w + NW, ... in its own LDS buffers,
+// the clip max / min are combined through LDS at one barrier, and the epilogue's 16 band blocks
+// are split over the waves.  Finer work units than one wave per clip shorten the tail of a
+// launch whose clip count is not a multiple of the resident clip-waves (config 2: 4096 clips on
+// 256 CUs x 12 waves).
+#ifndef FE_NW
+#define FE_NW 2
+#endif
+constexpr int NW = FE_NW;
+struct WaveBuf {
   int16_t win[WIN];                // reflect-padded window of the round, base = 160 f0 - 200
   cf st[R][200];                   // per frame: pass A out [k1][n2] -> Z[k] -> power rows
+};
+struct Smem {
+  WaveBuf w[NW];
   int zc[NF + 1];                  // ZCR counts of the clip
   uint8_t rb[NF + 1];              // image R byte per column
+  float red[2][NW];                // per-wave max / min of the mel power
 };
 static_assert(sizeof(int16_t) * WIN % 16 == 0, "st must stay 16-B aligned");
+static_assert(sizeof(WaveBuf) % 16 == 0, "wave buffers stay 16-B aligned");
 static_assert(P2W * sizeof(float2) <= 2 * 200 * sizeof(cf), "a pair's power row fits its FFT rows");
-MMLA_DEV float2* p2row(Smem& sm, int q) { return reinterpret_cast<float2*>(sm.st[2 * q]); }
+MMLA_DEV float2* p2row(WaveBuf& ws, int q) { return reinterpret_cast<float2*>(ws.st[2 * q]); }
 
 // |X[k]|^2 and |X[200 - k]|^2 of the 400-point real DFT from Z[k], Z[200 - k] of the packed FFT
 MMLA_DEV void split_power(cf z, cf zr, cf w, float& pk, float& pnk) {
@@ -215,10 +230,12 @@ template <bool DB, bool NM, bool IMG>
 #ifndef FE_MINB
 #define FE_MINB 3   // waves (= workgroups) per SIMD the register budget is sized for (12.5 KB LDS: 12 per CU)
 #endif
-__global__ void __launch_bounds__(NT, FE_MINB) od_fe_kernel(OdFeArgs a) {
+__global__ void __launch_bounds__(NT * NW, FE_MINB) od_fe_kernel(OdFeArgs a) {
   __shared__ __attribute__((aligned(16))) Smem sm;
   const OdFeTables& tb = *a.tables;
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & (NT - 1);
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / NT);
+  WaveBuf& ws = sm.w[wid];
   const int64_t clip = blockIdx.x;
 
   int len = a.lens ? a.lens[clip] : a.clip_len;
@@ -250,7 +267,7 @@ __global__ void __launch_bounds__(NT, FE_MINB) od_fe_kernel(OdFeArgs a) {
     nx1 = s4_[lane + NT];                                                                 \
     nx2 = s4_[l2 ? lane + 2 * NT : WCH - 1];   /* unconditional: a static load count */   \
   } while (0)
-  if (fast(0)) FE_PREFETCH(0);
+  if (fast(wid)) FE_PREFETCH(wid);
 
   // this lane's two mel bands: first bin and the band's taps (zero past its non-zeros)
   const int mlo = tb.mel_start[lane], mhi = tb.mel_start[lane + 64];
@@ -286,13 +303,13 @@ __global__ void __launch_bounds__(NT, FE_MINB) od_fe_kernel(OdFeArgs a) {
   static_assert(R % 2 == 0, "frame pairs");
 
   float smax = 0.0f, smin = INFINITY;
-  for (int r = 0; r < NR; ++r) {
+  for (int r = wid; r < NR; r += NW) {
     const int f0 = r * R;
     const int base = HOP * f0 - N_FFT / 2;
     lds_order();   // the previous round's mel reads of st are issued
     // ---- window: reflect padding for the STFT (centre=True, pad_mode='reflect') ------------------
     if (fast(r)) {
-      uint4* w4 = reinterpret_cast<uint4*>(sm.win);
+      uint4* w4 = reinterpret_cast<uint4*>(ws.win);
       w4[lane] = nx0;
       w4[lane + NT] = nx1;
       if (l2) w4[lane + 2 * NT] = nx2;
@@ -310,9 +327,9 @@ __global__ void __launch_bounds__(NT, FE_MINB) od_fe_kernel(OdFeArgs a) {
       }
 #pragma unroll
       for (int j = 0; j < SPL; ++j)
-        if (lane + NT * j < WIN) sm.win[lane + NT * j] = v[j];
+        if (lane + NT * j < WIN) ws.win[lane + NT * j] = v[j];
     }
-    if (r + 1 < NR && fast(r + 1)) FE_PREFETCH(r + 1);
+    if (r + NW < NR && fast(r + NW)) FE_PREFETCH(r + NW);
     lds_order();
     FE_MARK(0);
     // ---- zero crossings (edge padding, signbit semantics): lane l < 60 owns window positions
@@ -325,7 +342,7 @@ __global__ void __launch_bounds__(NT, FE_MINB) od_fe_kernel(OdFeArgs a) {
       int cl = 0, first = 0;
       if (lane < ZL) {
         const int w0 = ZCH * lane;
-        const uint2* wp = reinterpret_cast<const uint2*>(sm.win + w0);   // 40 B per lane
+        const uint2* wp = reinterpret_cast<const uint2*>(ws.win + w0);   // 40 B per lane
         uint32_t m = 0;                              // bit j: signbit of window sample w0 + j
 #pragma unroll
         for (int k = 0; k < ZCH / 4; ++k) {
@@ -336,7 +353,7 @@ __global__ void __launch_bounds__(NT, FE_MINB) od_fe_kernel(OdFeArgs a) {
           m |= (nib & 0xfu) << (4 * k);
         }
         // bit j of e: signbit of the sample at w0 - 1 + j (j = 0..20)
-        uint32_t e = (m << 1) | (w0 > 0 ? (uint32_t)(sm.win[w0 - 1] < 0) : 0u);
+        uint32_t e = (m << 1) | (w0 > 0 ? (uint32_t)(ws.win[w0 - 1] < 0) : 0u);
         const int i0 = base + w0 - 1;                // clip index of bit 0
         if (i0 < 0 || i0 + ZCH >= CLIP) {            // edge padding outside the clip
           const int nlo = min(max(-i0, 0), ZCH + 1);
@@ -349,7 +366,7 @@ __global__ void __launch_bounds__(NT, FE_MINB) od_fe_kernel(OdFeArgs a) {
         cl = __builtin_popcount(t);
         first = (int)(t & 1u);
       }
-      int* scan = reinterpret_cast<int*>(sm.st);   // st is free until pass A writes it
+      int* scan = reinterpret_cast<int*>(ws.st);   // st is free until pass A writes it
       scan[lane] = cl;
       scan[NT + lane] = first;
       lds_order();
@@ -371,7 +388,7 @@ __global__ void __launch_bounds__(NT, FE_MINB) od_fe_kernel(OdFeArgs a) {
     //      -> st[f][k1][n2] (the twiddle W200^(n2 k1) is applied by pass B) ---------------------------
     if (lane < R * 10) {
       const int f = lane / 10, n2 = lane - 10 * f;
-      const uint32_t* wp = reinterpret_cast<const uint32_t*>(sm.win) + 80 * f + n2;
+      const uint32_t* wp = reinterpret_cast<const uint32_t*>(ws.win) + 80 * f + n2;
       cf u[20];
 #pragma unroll
       for (int n1 = 0; n1 < 20; ++n1) {
@@ -380,7 +397,7 @@ __global__ void __launch_bounds__(NT, FE_MINB) od_fe_kernel(OdFeArgs a) {
         u[n1] = {(float)(int)(int16_t)(w & 0xffffu) * h.x, (float)((int)w >> 16) * h.y};
       }
       dft20(u);
-      cf* dst = &sm.st[f][n2];
+      cf* dst = &ws.st[f][n2];
 #pragma unroll
       for (int k1 = 0; k1 < 20; ++k1) dst[10 * k1] = u[k1];
     }
@@ -393,7 +410,7 @@ __global__ void __launch_bounds__(NT, FE_MINB) od_fe_kernel(OdFeArgs a) {
     for (int rr = 0; rr < 2; ++rr) {
       if (lane < 60) {
         const int f = 3 * rr + lane / 20, k1 = lane % 20;
-        const float4* row = reinterpret_cast<const float4*>(&sm.st[f][10 * k1]);
+        const float4* row = reinterpret_cast<const float4*>(&ws.st[f][10 * k1]);
         cf v[10];
 #pragma unroll
         for (int j = 0; j < 5; ++j) {
@@ -406,7 +423,7 @@ __global__ void __launch_bounds__(NT, FE_MINB) od_fe_kernel(OdFeArgs a) {
         for (int j = 1; j < 10; ++j) v[j] = cmul(v[j], tk[j]);
         dft10(v);
 #pragma unroll
-        for (int k2 = 0; k2 < 10; ++k2) sm.st[f][k1 + 20 * k2] = v[k2];
+        for (int k2 = 0; k2 < 10; ++k2) ws.st[f][k1 + 20 * k2] = v[k2];
       }
       lds_order();
     }
@@ -420,7 +437,7 @@ __global__ void __launch_bounds__(NT, FE_MINB) od_fe_kernel(OdFeArgs a) {
       cf za[2], zar[2], zb[2] = {{0.f, 0.f}, {0.f, 0.f}}, zbr[2] = {{0.f, 0.f}, {0.f, 0.f}};
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
-        const cf* Z = sm.st[2 * q + c];
+        const cf* Z = ws.st[2 * q + c];
         za[c] = Z[ka];
         zar[c] = Z[ka == 0 ? 0 : 200 - ka];
         if (hb) {
@@ -429,7 +446,7 @@ __global__ void __launch_bounds__(NT, FE_MINB) od_fe_kernel(OdFeArgs a) {
         }
       }
       lds_order();
-      float* P = reinterpret_cast<float*>(p2row(sm, q));   // P[2q + c][k] at P[2 k + c]
+      float* P = reinterpret_cast<float*>(p2row(ws, q));   // P[2q + c][k] at P[2 k + c]
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
         float p0, p1;
@@ -454,7 +471,7 @@ __global__ void __launch_bounds__(NT, FE_MINB) od_fe_kernel(OdFeArgs a) {
     float s0 = 0.0f, s1 = 0.0f;
 #pragma unroll
     for (int q = 0; q < R / 2; ++q) {
-      const float2* P = p2row(sm, q);
+      const float2* P = p2row(ws, q);
       float2 a0 = {0.0f, 0.0f}, a1 = {0.0f, 0.0f};
 #pragma unroll
       for (int j = 0; j < T_LO; ++j) {
@@ -490,7 +507,18 @@ __global__ void __launch_bounds__(NT, FE_MINB) od_fe_kernel(OdFeArgs a) {
   smax = wave_max(smax);
   smin = wave_min(smin);
   wave_stores_done();   // this wave's scratch stores have completed (common.h)
-  lds_order();
+  if (lane == 0) {
+    sm.red[0][wid] = smax;
+    sm.red[1][wid] = smin;
+  }
+  __syncthreads();      // every wave's scratch rows, ZCR counts and max / min are in place
+  smax = sm.red[0][0];
+  smin = sm.red[1][0];
+#pragma unroll
+  for (int w = 1; w < NW; ++w) {
+    smax = fmaxf(smax, sm.red[0][w]);
+    smin = fminf(smin, sm.red[1][w]);
+  }
 
   // power_to_db(ref=np.max, amin=1e-10, top_db=80) with numpy-1.21 dtypes, then normalize_matrix.
   // log10 is monotone, so max/min of the dB matrix are the dB of max/min S.  Each numpy op rounds
@@ -506,18 +534,20 @@ __global__ void __launch_bounds__(NT, FE_MINB) od_fe_kernel(OdFeArgs a) {
   float* db_out = a.db + clip * (NMEL * NF);      // dereferenced only when DB
   float* nm_out = a.norm + clip * (NMEL * NF);    // only when NM
   if (a.zcr) {
-    for (int f = lane; f < NF; f += NT) a.zcr[clip * NF + f] = (float)sm.zc[f] * (1.0f / 400.0f);
+    for (int f = threadIdx.x; f < NF; f += NT * NW) a.zcr[clip * NF + f] = (float)sm.zc[f] * (1.0f / 400.0f);
   }
   // LDS of the round loop is free: [8][151] band-major tiles of normalised / dB values, i.e. the
   // output layout itself (a block of 8 bands is 1208 contiguous floats of [128][151])
   constexpr int MB = 8;                                    // bands per column block
   constexpr int BLK = MB * NF;                             // 1208 floats = 302 float4
-  float* nvt = reinterpret_cast<float*>(sm.win);           // [MB][NF] over win + st
+  float* nvt = reinterpret_cast<float*>(ws.win);           // [MB][NF] over the wave's win + st
   float* dbt = nvt + BLK;                                  // [MB][NF]
-  static_assert(sizeof(sm.win) + sizeof(sm.st) >= 2 * BLK * sizeof(float), "LDS tiles");
-  static_assert(sizeof(sm.win) % 16 == 0 && BLK % 4 == 0, "16-B tile rows");
-  if (IMG)
-    for (int w = lane; w < NF; w += NT) sm.rb[w] = (uint8_t)(int)(((double)sm.zc[w] / 400.0) * 255.0);
+  static_assert(sizeof(WaveBuf) >= 2 * BLK * sizeof(float), "LDS tiles");
+  static_assert(BLK % 4 == 0, "16-B tile rows");
+  if (IMG) {
+    for (int w = threadIdx.x; w < NF; w += NT * NW) sm.rb[w] = (uint8_t)(int)(((double)sm.zc[w] / 400.0) * 255.0);
+    __syncthreads();
+  }
   const float inv_diff = 1.0f / diff;
   // the block's scratch reads are issued one block ahead (registers); with static store counts the
   // compiler's wait for them is vmcnt(N), not a drain of the previous block's output stores
@@ -531,11 +561,12 @@ __global__ void __launch_bounds__(NT, FE_MINB) od_fe_kernel(OdFeArgs a) {
       nx[q_] = *reinterpret_cast<const float4*>(scr + t_ * NMEL + MB * (mb_) + 4 * qd_);       \
     }                                                                                          \
   } while (0)
-  FE_FETCH(0);
-  for (int mb = 0; mb < NMEL / MB; ++mb) {
+  static_assert((NMEL / MB) % NW == 0, "band blocks per wave");
+  FE_FETCH(wid);
+  for (int mb = wid; mb < NMEL / MB; mb += NW) {
 #pragma unroll
     for (int q = 0; q < RPL; ++q) cur[q] = nx[q];
-    if (mb + 1 < NMEL / MB) FE_FETCH(mb + 1);
+    if (mb + NW < NMEL / MB) FE_FETCH(mb + NW);
     lds_order();   // the previous block's tile reads are issued
 #pragma unroll
     for (int q = 0; q < RPL; ++q) {                           // frame t, quad of bands
@@ -620,7 +651,7 @@ bool od_fe_tables_ok(const OdFeTables& t) {
 }
 
 static void launch_v2(const OdFeArgs& a, int64_t n, hipStream_t s) {
-  const dim3 g((unsigned)n), b(NT);
+  const dim3 g((unsigned)n), b(NT * v2::NW);
   const int k = (a.db ? 4 : 0) | (a.norm ? 2 : 0) | (a.img ? 1 : 0);
   switch (k) {
     case 0: hipLaunchKernelGGL((v2::od_fe_kernel<false, false, false>), g, b, 0, s, a); break;
