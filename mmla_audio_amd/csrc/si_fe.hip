@@ -70,12 +70,17 @@ constexpr int LFE = PART + 2 * SI_FE_MAX_SUB;   // then 27 log energies
 static_assert(LFE + 27 <= 2 * FP, "frame region");
 static_assert(NL * 13 * sizeof(float) <= R * FP * sizeof(cd), "epilogue cepstra tile");
 
-struct Smem {                   // 19.7 KB
-  int16_t win[WIN];             // x[160 g0 - 8 + w] (0 outside [0, len))
-  cd z[R][FP];                  // pass A rows [k1][17] -> Z[k] -> P[k] (doubles) + sums + logs
+struct Smem {                   // 18.7 KB: 8 clip-waves per CU
+  // pass A rows [k1][17] -> Z[k] -> P[k] (doubles) + sums + logs.  The round's window
+  // x[160 g0 - 8 + w] (0 outside [0, len)) is staged over the start of z: pass A issues all of its
+  // window reads before its first row store, and nothing else reads the window
+  cd z[R][FP];
   double s2[R];                 // sum of the frame's squared pre-emphasised samples
   float ext[2 * HALO][13];      // cepstra of local frames 0..3 and 260..263 (not output rows)
+  double dct[12][13];           // lifted DCT-II rows 1..12, folded (26 -> 13 terms)
 };
+static_assert(WIN * sizeof(int16_t) <= sizeof(cd) * R * FP, "window inside z");
+MMLA_DEV int16_t* win_of(Smem& sm) { return reinterpret_cast<int16_t*>(&sm.z[0][0]); }
 
 // W16^e = exp(-2 pi i e / 16)
 constexpr double C8 = 0.92387953251128675613, S8 = 0.38268343236508977173, RH = 0.70710678118654752440;
@@ -116,7 +121,10 @@ MMLA_DEV void split_power(cd z, cd zr, cd w, double& pk, double& pnk) {
   pnk = (xm.x * xm.x + xm.y * xm.y) * (1.0 / 512.0);
 }
 
-__global__ void __launch_bounds__(NT, 2) si_fe_kernel(SiFeArgs a) {
+#ifndef SI_MINB
+#define SI_MINB 2
+#endif
+__global__ void __launch_bounds__(NT, SI_MINB) si_fe_kernel(SiFeArgs a) {
   __shared__ __attribute__((aligned(16))) Smem sm;
   const SiFeTables& tb = *a.tables;
   const int lane = threadIdx.x;
@@ -161,18 +169,15 @@ __global__ void __launch_bounds__(NT, 2) si_fe_kernel(SiFeArgs a) {
   const cd wb = {tb.w512[lane + 64][0], tb.w512[lane + 64][1]};
   // sub-segment tasks t = lane + 64 s -> (frame, sub-segment)
   const int n_sub = tb.n_sub;
-  int sf[3], sst[3], scn[3], su[3];
-  double sd0[3];
+  // packed into one register each (the kernel sits at the register limit): first bin [0, 9),
+  // count [9, 13), frame [13, 15), sub-segment [15, 21), offset in its segment [21, 30)
+  int stask[3];
 #pragma unroll
   for (int s = 0; s < 3; ++s) {
     const int t = lane + NT * s;
     const bool on = t < R * n_sub;
     const int f = on ? t / n_sub : 0, u = on ? t - f * n_sub : 0;
-    sf[s] = f;
-    su[s] = u;
-    sst[s] = tb.sub_start[u];
-    scn[s] = on ? tb.sub_cnt[u] : 0;
-    sd0[s] = (double)tb.sub_d0[u];
+    stask[s] = tb.sub_start[u] | (on ? tb.sub_cnt[u] : 0) << 9 | f << 13 | u << 15 | tb.sub_d0[u] << 21;
   }
   // filter tasks (lane < 52): filter j of frames lane / 26 and 2 + lane / 26; lanes 52..55: energy
   const int fj = lane % 26;
@@ -182,9 +187,9 @@ __global__ void __launch_bounds__(NT, 2) si_fe_kernel(SiFeArgs a) {
   const int dcf = lane < 48 ? lane / 12 : lane - 48, dcc = lane < 48 ? 1 + lane % 12 : 0;
   // DCT-II rows are (anti)symmetric: dct[c][25 - j] = (-1)^c dct[c][j] -> 13 coefficients, and the
   // dot product folds the log energies pairwise first
-  double dct[13];
-#pragma unroll
-  for (int j = 0; j < 13; ++j) dct[j] = tb.dct[dcc][j];
+  // (in LDS: as 13 registers per lane they were spilled to scratch, and every reload waited for
+  // all of the wave's outstanding window loads and cepstra stores)
+  for (int e = lane; e < 12 * 13; e += NT) sm.dct[e / 13][e % 13] = tb.dct[1 + e / 13][e % 13];
   const double dsg = (dcc & 1) ? -1.0 : 1.0;
 
   // ---- the round's window: register prefetch one round ahead when it lies inside [0, len) --------
@@ -209,7 +214,7 @@ __global__ void __launch_bounds__(NT, 2) si_fe_kernel(SiFeArgs a) {
     const bool fr = fast(g0);
     lds_order();   // the previous round's reads of win / z are issued
     if (fr) {
-      uint4* w4 = reinterpret_cast<uint4*>(sm.win);
+      uint4* w4 = reinterpret_cast<uint4*>(win_of(sm));
       w4[lane] = nx0;
       if (l1) w4[lane + NT] = nx1;
     } else {
@@ -223,14 +228,14 @@ __global__ void __launch_bounds__(NT, 2) si_fe_kernel(SiFeArgs a) {
       }
 #pragma unroll
       for (int j = 0; j < SPL; ++j)
-        if (lane + NT * j < WIN) sm.win[lane + NT * j] = v[j];
+        if (lane + NT * j < WIN) win_of(sm)[lane + NT * j] = v[j];
     }
     if (r + 1 < nr && fast(g0 + R)) SI_PREFETCH(g0 + R);
     lds_order();
 
     // ---- pass A: z[n] = s[2n] + i s[2n+1], n = 16 n1 + q (< 200: 400-sample frame in 512) ----------
     {
-      const uint32_t* wv = reinterpret_cast<const uint32_t*>(sm.win) + 4 + 80 * fq + q;
+      const uint32_t* wv = reinterpret_cast<const uint32_t*>(win_of(sm)) + 4 + 80 * fq + q;
       const int64_t lim = len - (160 * (g0 + fq) + 2 * q);   // s[2n] exists iff 32 n1 < lim
       cd v[16];
       double e2 = 0.0;
@@ -306,18 +311,21 @@ __global__ void __launch_bounds__(NT, 2) si_fe_kernel(SiFeArgs a) {
     // ---- sub-segment sums: A = sum P[k], B = sum (k - bin[s]) P[k] = sum i P + d0 A -------------------
 #pragma unroll
     for (int s = 0; s < 3; ++s) {
-      if (scn[s] > 0) {
-        double* Q = reinterpret_cast<double*>(sm.z[sf[s]]);
-        const double* p = Q + sst[s];
+      const int scn = (stask[s] >> 9) & 15;
+      if (scn > 0) {
+        double* Q = reinterpret_cast<double*>(sm.z[(stask[s] >> 13) & 3]);
+        const double* p = Q + (stask[s] & 511);
         double A = 0.0, B = 0.0;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
           const double v = p[i];                 // past the sub-segment: finite LDS words, not used
-          const double pv = i < scn[s] ? v : 0.0;
+          const double pv = i < scn ? v : 0.0;
           A += pv;
           if (i > 0) B = fma((double)i, pv, B);
         }
-        reinterpret_cast<double2*>(Q + PART)[su[s]] = double2{A, fma(sd0[s], A, B)};
+        int d0 = (stask[s] >> 21) & 511;
+        asm volatile("" : "+v"(d0));   // converted here: a hoisted double of it was spilled
+        reinterpret_cast<double2*>(Q + PART)[(stask[s] >> 15) & 63] = double2{A, fma((double)d0, A, B)};
       }
     }
     lds_order();
@@ -360,7 +368,7 @@ __global__ void __launch_bounds__(NT, 2) si_fe_kernel(SiFeArgs a) {
       if (lane < 48) {
         v = 0.0;
 #pragma unroll
-        for (int j = 0; j < 13; ++j) v = fma(fma(dsg, L[25 - j], L[j]), dct[j], v);
+        for (int j = 0; j < 13; ++j) v = fma(fma(dsg, L[25 - j], L[j]), sm.dct[dcc - 1][j], v);
       } else {
         v = L[26];
       }
