@@ -106,9 +106,27 @@ template <class S> MMLA_DEV constexpr int shp_w() { return ShapeOf<S>::w; }
 template <class S> MMLA_DEV constexpr int shp_ci() { return ShapeOf<S>::ci; }
 template <class S> MMLA_DEV constexpr int shp_co() { return ShapeOf<S>::co; }
 
+// Waves per SIMD the register budget is sized for: 3 (<= 168 VGPRs) for the SI Conv1D BN 128 tiles
+// (the residual variant needed 169 and ran at 2; now 168 + 2 spilled dwords) and for the fixed-shape
+// 64-channel residual conv(4,1) of OD blocks 5-6 (172 -> 166 VGPRs, 44.8 KB LDS: 3 workgroups per
+// CU); conv -0.4 % (OD) / -0.5 % (SI) per step in an A/B.  2 elsewhere: forced to 3, the block-4
+// conv(4,1) + pool and the 19-wide BN 128 layers spill 64-152 B per lane.
+#ifndef CONV_MINW_SI
+#define CONV_MINW_SI 3
+#endif
+#ifndef CONV_MINW_R64
+#define CONV_MINW_R64 3
+#endif
+template <int KH, int BN, int TW, int EPI, bool FIXED>
+constexpr int conv_minw() {
+  return TW == 1 && BN == 128                                       ? CONV_MINW_SI
+         : (FIXED && KH == 4 && BN == 64 && TW == 8 && EPI == EPI_ADD) ? CONV_MINW_R64
+                                                                     : 2;
+}
+
 template <int KH, int KW, int CK, int BN, int TW, int PRO, int EPI, bool POOL, bool V4 = true,
           bool PIN = false, class SHP = Shape<0, 0, 0, 0>>
-__global__ void __launch_bounds__(NT, 2) conv_h3_kernel(ConvH3Args a) {
+__global__ void __launch_bounds__(NT, (conv_minw<KH, BN, TW, EPI, SHP::FIXED>())) conv_h3_kernel(ConvH3Args a) {
   // each wave owns ONE 32-column slice of B (no B fragment is loaded by two waves) and
   // 128 / WM rows: BN 32 -> 4 x 1, BN 64 -> 2 x 2, BN 128 -> 1 x 4 (waves along N)
   constexpr int WN = BN / 32;
