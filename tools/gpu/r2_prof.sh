@@ -4,9 +4,10 @@ cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 wl=${WL:-od_pipeline}; tag=${TAG:-$wl}
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$tag -o run -- python3 bench.py --workload $wl --no-cpu-baseline --no-f32 --no-parity ${BENCH_ARGS} > gpurun_out/prof_$tag.log 2>&1 || { tail -20 gpurun_out/prof_$tag.log; exit 1; }
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$tag -o run -- python3 bench.py --workload $wl --no-cpu-baseline --no-f32 --no-parity ${BENCH_ARGS} > gpurun_out/prof_$tag.log 2>&1 || { tail -20 gpurun_out/prof_$tag.log; exit 1; }
 f=$(find gpurun_out/prof_$tag -name '*kernel_stats.csv' | head -1)
 cp $f gpurun_out/${tag}_kernel_stats.csv
+rm -rf gpurun_out/prof_$tag   # traces exceed gpurun's copy-back limit
 python3 - <<PY
 import csv
 rows=list(csv.DictReader(open('gpurun_out/${tag}_kernel_stats.csv')))
