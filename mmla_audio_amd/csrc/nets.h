@@ -21,7 +21,7 @@ hipError_t bilstm_launch(const float* seq, int n, int T, int D, const float* wca
                          const float* wcat_bwd, const float* bias_fwd, const float* bias_bwd,
                          float* out, hipStream_t s);
 // The same BiLSTM on the f16 MFMA with 3xFP16 products (error-compensated hi/lo splits, f32
-// accumulation); w*h / w*l = bilstm_h3_split_weights(wcat): [1024][256 + D] fp16 bits.
+// accumulation); w*h / w*l = bilstm_h3_split_weights(wcat): 1024 x (256 + D) fp16 bits in MFMA fragment order.
 hipError_t bilstm_h3_launch(const float* seq, int n, int T, int D, const uint16_t* wfh,
                             const uint16_t* wfl, const uint16_t* wbh, const uint16_t* wbl,
                             const float* bias_fwd, const float* bias_bwd, float* out,

@@ -233,10 +233,15 @@ __global__ void __launch_bounds__(512) bilstm_h3_kernel(const float* __restrict_
   }
   const int col = 32 * wave + (lane & 31);   // hidden unit of this lane's accumulator column
   const int koff = 8 * (lane >> 5);
-  // gate g's B rows: (g * 256 + col) * K + koff; g advances by 256 * K
-  const uint16_t* wh0 = Wh + (size_t)col * K + koff;
-  const uint16_t* wl0 = Wl + (size_t)col * K + koff;
+  // B in MFMA fragment order (bilstm_h3_split_weights): the wave's 64 16-B fragments of one gate and
+  // k-step are 1 KB contiguous, so a load instruction fills 8 whole 128-B lines.  (Column-major B
+  // put the 64 lanes on 32 lines 768 B apart and used 32 B of each: the L1 could not hold the
+  // 256 KB of lines a k-step touched, so every 128-B line came from L2 four times.)
+  // gate g: + g * GS; k-step ks: + 512 * ks
+  const uint16_t* wh0 = Wh + (size_t)wave * KST * 512 + lane * 8;
+  const uint16_t* wl0 = Wl + (size_t)wave * KST * 512 + lane * 8;
   constexpr size_t GS = (size_t)LSTM_U * K;
+  static_assert(GS == (size_t)(LSTM_U / 32) * KST * 512, "fragment-major gate stride");
   const _Float16* arow_h = Ahi + (lane & 31) * LDA + koff;
   const _Float16* arow_l = Alo + (lane & 31) * LDA + koff;
   float cst[MT][16];
@@ -290,14 +295,14 @@ __global__ void __launch_bounds__(512) bilstm_h3_kernel(const float* __restrict_
         const int kn = ks + 1 < KST ? ks + 1 : ks;
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-          nh[g] = *reinterpret_cast<const f16x8*>(wh0 + g * GS + 16 * kn);
-          nl[g] = *reinterpret_cast<const f16x8*>(wl0 + g * GS + 16 * kn);
+          nh[g] = *reinterpret_cast<const f16x8*>(wh0 + g * GS + 512 * kn);
+          nl[g] = *reinterpret_cast<const f16x8*>(wl0 + g * GS + 512 * kn);
         }
       } else {
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-          bh[g] = *reinterpret_cast<const f16x8*>(wh0 + g * GS + 16 * ks);
-          bl[g] = *reinterpret_cast<const f16x8*>(wl0 + g * GS + 16 * ks);
+          bh[g] = *reinterpret_cast<const f16x8*>(wh0 + g * GS + 512 * ks);
+          bl[g] = *reinterpret_cast<const f16x8*>(wl0 + g * GS + 512 * ks);
         }
       }
 #pragma unroll
@@ -484,14 +489,20 @@ bool bilstm_h3_weights_in_range(const float* wcat, int D) {
 }
 
 void bilstm_h3_split_weights(const float* wcat, int D, uint16_t* hi, uint16_t* lo) {
-  const int K = 256 + D;
+  // MFMA fragment order: gate column j = 256 g + 32 w + n (w: the wave owning it), k = 16 ks + 8 hf +
+  // e -> ((g * 8 + w) * KST + ks) * 512 + (n + 32 hf) * 8 + e, i.e. the B fragment of lane
+  // n + 32 hf for that gate / wave / k-step (bilstm_h3_kernel)
+  const int K = 256 + D, KST = K / 16;
   for (int j = 0; j < 1024; ++j)
     for (int k = 0; k < K; ++k) {
       const float v = wcat[(size_t)k * 1024 + j] * LSTM_WS;   // exact power-of-two scale
       const _Float16 h = (_Float16)v;
       const _Float16 l = (_Float16)(v - (float)h);   // not rescaled (bilstm_h3_kernel)
-      memcpy(&hi[(size_t)j * K + k], &h, 2);
-      memcpy(&lo[(size_t)j * K + k], &l, 2);
+      const int g = j / 256, w = (j % 256) / 32, n = j % 32;
+      const int ks = k / 16, hf = (k % 16) / 8, e = k % 8;
+      const size_t at = ((size_t)(g * 8 + w) * KST + ks) * 512 + (size_t)(n + 32 * hf) * 8 + e;
+      memcpy(&hi[at], &h, 2);
+      memcpy(&lo[at], &l, 2);
     }
 }
 
