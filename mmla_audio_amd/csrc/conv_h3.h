@@ -25,6 +25,7 @@ struct ConvH3Args {
 
 // Picks the tile and launches; returns hipErrorInvalidValue for unsupported shapes.
 hipError_t conv_h3_launch(ConvH3Args a, hipStream_t stream);
-// Host: split float32 weights [kh,kw,cin,cout] into the fp16 hi/lo [tap][cout_pad][cin_pad] layout.
+// Host: split float32 weights [kh,kw,cin,cout] into fp16 hi/lo, per tap in MFMA fragment order
+// [cin_pad / 16][cout_pad / 32][64 lanes][8] (conv_h3_kernel).
 void conv_h3_split_weights(const float* w, int kh, int kw, int cin, int cout, int cin_pad,
                            int cout_pad, uint16_t* hi, uint16_t* lo);

@@ -228,15 +228,15 @@ __global__ void __launch_bounds__(NT, (conv_minw<KH, BN, TW, EPI, SHP::FIXED>())
 #pragma unroll
       for (int i = 0; i < 16; ++i) acc[mt][nt][i] = 0.0f;
 
-  const uint16_t* whp[NTL];
-  const uint16_t* wlp[NTL];
+  // B in MFMA fragment order (conv_h3_split_weights): per tap, 16-channel k-step and 32-channel
+  // output tile the 64 lanes' 16-B fragments are 1 KB contiguous, so one load instruction covers 8
+  // whole 128-B lines (the [co][ci] rows had put a wave's 64 lanes on 32 lines, 32 B used of each)
+  // (address = wave-uniform base + a 32-bit lane offset, so the loads take the scalar-base form)
+  int lofs[NTL];
 #pragma unroll
-  for (int nt = 0; nt < NTL; ++nt) {
-    const int co = n0 + (wn * NTL + nt) * 32 + (lane & 31);
-    whp[nt] = a.wh + (size_t)co * A_CINP + koff;
-    wlp[nt] = a.wl + (size_t)co * A_CINP + koff;
-  }
+  for (int nt = 0; nt < NTL; ++nt) lofs[nt] = (n0 / 32 + wn * NTL + nt) * 512 + lane * 8;
   const size_t tap_stride = (size_t)A_COUTP * A_CINP;
+  const size_t kstride = (size_t)(A_COUTP / 32) * 512;   // one 16-channel k-step
   // the epilogue's bias, loaded now: after the MFMA loop it cost a memory round trip of its own
   float bias_r[NTL];
 #pragma unroll
@@ -312,8 +312,9 @@ __global__ void __launch_bounds__(NT, (conv_minw<KH, BN, TW, EPI, SHP::FIXED>())
       for (int nt = 0; nt < NTL; ++nt)
 #pragma unroll
         for (int s = 0; s < KS; ++s) {
-          bh[nt][s] = *reinterpret_cast<const f16x8*>(whp[nt] + ci0 + 16 * s);
-          bl[nt][s] = *reinterpret_cast<const f16x8*>(wlp[nt] + ci0 + 16 * s);
+          const size_t u = (size_t)(ch * KS + s) * kstride;
+          bh[nt][s] = *reinterpret_cast<const f16x8*>(a.wh + u + lofs[nt]);
+          bl[nt][s] = *reinterpret_cast<const f16x8*>(a.wl + u + lofs[nt]);
         }
     };
     if constexpr (EARLY_B) load_b0();
@@ -379,8 +380,9 @@ __global__ void __launch_bounds__(NT, (conv_minw<KH, BN, TW, EPI, SHP::FIXED>())
         for (int nt = 0; nt < NTL; ++nt)
 #pragma unroll
           for (int s = 0; s < KS; ++s) {
-            nbh[nt][s] = *reinterpret_cast<const f16x8*>(whp[nt] + (tap + 1) * tap_stride + ci0 + 16 * s);
-            nbl[nt][s] = *reinterpret_cast<const f16x8*>(wlp[nt] + (tap + 1) * tap_stride + ci0 + 16 * s);
+            const size_t u = (tap + 1) * tap_stride + (size_t)(ch * KS + s) * kstride;
+            nbh[nt][s] = *reinterpret_cast<const f16x8*>(a.wh + u + lofs[nt]);
+            nbl[nt][s] = *reinterpret_cast<const f16x8*>(a.wl + u + lofs[nt]);
           }
       }
 #pragma unroll
@@ -732,7 +734,10 @@ void conv_h3_split_weights(const float* w, int kh, int kw, int cin, int cout, in
       for (int co = 0; co < cout; ++co) {
         const float v = w[((size_t)t * cin + ci) * cout + co] * W_SCALE;   // exact
         const _Float16 h = (_Float16)v;
-        const size_t o = ((size_t)t * cout_pad + co) * cin_pad + ci;
+        // MFMA fragment order: [tap][ci / 16][co / 32][lane = co % 32 + 32 (ci % 16 / 8)][ci % 8]
+        const size_t o = (size_t)t * cout_pad * cin_pad +
+                         (((size_t)(ci / 16) * (cout_pad / 32) + co / 32) * 64 + co % 32 +
+                          32 * ((ci % 16) / 8)) * 8 + ci % 8;
         hi[o] = f32_to_f16_bits(v);
         lo[o] = f32_to_f16_bits(v - (float)h);
       }
