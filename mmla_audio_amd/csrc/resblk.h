@@ -35,6 +35,6 @@ int resblk_k1pad(int cin);
 bool resblk_supported(int cin, int c, bool pool);
 hipError_t resblk_launch(ResBlkArgs a, int cin, int c, bool pool, hipStream_t stream);
 // Host: float32 Keras weights [taps][cin][cout] -> fp16 hi/lo [cout][kpad] with k = tap * cin + ci
-// (zero for k >= taps * cin).
+// (zero for k >= taps * cin); frag: GEMM 1's MFMA fragment order [k / 32][cout / 16][64 lanes][8].
 void resblk_split_weights(const float* w, int taps, int cin, int cout, int kpad, uint16_t* hi,
-                          uint16_t* lo);
+                          uint16_t* lo, bool frag);

@@ -140,7 +140,7 @@ template <int CIN, int C, bool POOL, bool STEM>
 __global__ void __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(ResBlkArgs a) {
   using G = Geo<CIN, C, POOL>;
   constexpr int XC = G::XC, XPS = G::XPS, TPS = G::TPS, MT1 = G::MT1, MT2 = G::MT2, NTW = G::NTW;
-  constexpr int KS1 = G::KS1, K1PAD = G::K1PAD, KS2 = G::KS2, PF = G::PF, QPP = G::QPP;
+  constexpr int KS1 = G::KS1, KS2 = G::KS2, PF = G::PF, QPP = G::QPP;
   constexpr int MAXT = G::MAXT, WN = G::WN;
   // [halo | t1] (hi and lo, layouts in Geo), then GEMM 2's weights hi, lo
   __shared__ __attribute__((aligned(16))) _Float16 smem[G::SM + 2 * G::W2];
@@ -279,14 +279,18 @@ __global__ void __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(R
   }
 
   // GEMM 1's first PF k-steps of B: in flight across the staging and its barrier
-  const int b1o = ((wn * NTW) * 16 + col) * K1PAD + 8 * grp;   // + nt * 16 * K1PAD
+  // GEMM 1's B in MFMA fragment order (resblk_split_weights, frag): per 32-deep k-step and 16-channel
+  // tile the 64 lanes' 16-B fragments are 1 KB contiguous (8 whole 128-B lines per load instead of
+  // 16 rows at 64 B each)
+  const int b1o = (wn * NTW) * 512 + lane * 8;   // + nt * 512 + s * B1KS
+  constexpr int B1KS = (C / 16) * 512;
   f16x8 bh[PF][NTW], bl[PF][NTW];   // ring of B fragments, PF k-steps ahead
 #pragma unroll
   for (int s = 0; s < PF && s < KS1; ++s)
 #pragma unroll
     for (int nt = 0; nt < NTW; ++nt) {
-      bh[s][nt] = *reinterpret_cast<const f16x8*>(a.w1h + b1o + nt * 16 * K1PAD + 32 * s);
-      bl[s][nt] = *reinterpret_cast<const f16x8*>(a.w1l + b1o + nt * 16 * K1PAD + 32 * s);
+      bh[s][nt] = *reinterpret_cast<const f16x8*>(a.w1h + b1o + nt * 512 + B1KS * s);
+      bl[s][nt] = *reinterpret_cast<const f16x8*>(a.w1l + b1o + nt * 512 + B1KS * s);
     }
 
   if constexpr (STEM) {
@@ -426,8 +430,8 @@ __global__ void __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(R
       if (s + PF < KS1) {
 #pragma unroll
         for (int nt = 0; nt < NTW; ++nt) {
-          bh[s % PF][nt] = *reinterpret_cast<const f16x8*>(a.w1h + b1o + nt * 16 * K1PAD + 32 * (s + PF));
-          bl[s % PF][nt] = *reinterpret_cast<const f16x8*>(a.w1l + b1o + nt * 16 * K1PAD + 32 * (s + PF));
+          bh[s % PF][nt] = *reinterpret_cast<const f16x8*>(a.w1h + b1o + nt * 512 + B1KS * (s + PF));
+          bl[s % PF][nt] = *reinterpret_cast<const f16x8*>(a.w1l + b1o + nt * 512 + B1KS * (s + PF));
         }
       }
 #pragma unroll
@@ -667,14 +671,17 @@ static uint16_t f16_bits(float f) {
 }
 
 void resblk_split_weights(const float* w, int taps, int cin, int cout, int kpad, uint16_t* hi,
-                          uint16_t* lo) {
+                          uint16_t* lo, bool frag) {
   for (size_t i = 0; i < (size_t)cout * kpad; ++i) hi[i] = lo[i] = 0;
   for (int t = 0; t < taps; ++t)
     for (int ci = 0; ci < cin; ++ci)
       for (int co = 0; co < cout; ++co) {
         const float v = w[((size_t)t * cin + ci) * cout + co] * W_SCALE;   // exact
         const _Float16 h = (_Float16)v;
-        const size_t o = (size_t)co * kpad + (size_t)t * cin + ci;
+        const size_t k = (size_t)t * cin + ci;
+        // frag: [k / 32][co / 16][lane = co % 16 + 16 (k % 32 / 8)][k % 8] (GEMM 1's B fragments)
+        const size_t o = frag ? (((k / 32) * (cout / 16) + co / 16) * 64 + co % 16 + 16 * ((k % 32) / 8)) * 8 + k % 8
+                              : (size_t)co * kpad + k;
         hi[o] = f16_bits(v);
         lo[o] = f16_bits(v - (float)h);
       }
