@@ -174,8 +174,8 @@ __global__ void __launch_bounds__(256) bilstm_kernel(const float* __restrict__ s
 // ---- 3xFP16 BiLSTM ----------------------------------------------------------------------------
 // The same recurrence with the [32 x 384] x [384 x 1024] step product on the f16 MFMA
 // (v_mfma_f32_32x32x16_f16) with 3xFP16 products: A = [h_{t-1} | x_t] split into fp16 hi/lo in LDS,
-// B = the stacked kernels pre-split on the host and TRANSPOSED to [1024 gate columns][384 k] so a
-// lane's 8 k-values are one 16-B load.  Unlike conv_h3 the lo halves are not rescaled by 2^11, so
+// B = the stacked kernels pre-split on the host and packed in MFMA fragment order (a lane's 8
+// k-values are one 16-B load, a wave's 64 loads one contiguous KB).  Unlike conv_h3 the lo halves are not rescaled by 2^11, so
 // hi*hi, hi*lo and lo*hi accumulate into ONE f32 accumulator per gate tile (the registers that frees
 // hold the next k-step's B fragments: the weight stream from L2 is what the step waits on); to keep
 // the lo halves out of the fp16 subnormals both operands are scaled by exact powers of two first
