@@ -155,10 +155,21 @@ __global__ void __launch_bounds__(NT, (conv_minw<KH, BN, TW, EPI, SHP::FIXED>())
   // the 3x3 and linear-pixel variants lose 2.5-6.6 % and the SI Conv1D stack 5 %.  The pooled
   // epilogue needs the pixel-row layout (its 2x2 windows inside one lane's registers).
   constexpr bool CIL = !POOL && EPI == EPI_ADD && TW == 8;
-  __shared__ __attribute__((aligned(16))) _Float16 lds_hi[NPIX * LDP];
-  __shared__ __attribute__((aligned(16))) _Float16 lds_lo[NPIX * LDP];
+  // Conv1D (TW == 1): one more staged row that stays zero -- a tap whose source row leaves the output
+  // row's clip reads it (one select of the row offset per tap and row tile, instead of zeroing the
+  // 2 x 8 halves of every A fragment read)
+  constexpr int ZROW = TW == 1 && KH > 1 ? 1 : 0;
+  __shared__ __attribute__((aligned(16))) _Float16 lds_hi[(NPIX + ZROW) * LDP];
+  __shared__ __attribute__((aligned(16))) _Float16 lds_lo[(NPIX + ZROW) * LDP];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if constexpr (ZROW) {   // read only after the first chunk's staging barrier
+    static_assert(LDP % 8 == 0 && LDP / 8 <= NT, "zero row");
+    if (tid < LDP / 8) {
+      *reinterpret_cast<f16x8*>(lds_hi + NPIX * LDP + 8 * tid) = f16x8{};
+      *reinterpret_cast<f16x8*>(lds_lo + NPIX * LDP + 8 * tid) = f16x8{};
+    }
+  }
 #if CH_EXP
   const unsigned long long ch_t0 = CH_T();
   unsigned long long ch_sum[5] = {0, 0, 0, 0, 0}, ch_a = 0, ch_b = 0, ch_c = 0;
@@ -389,16 +400,14 @@ __global__ void __launch_bounds__(NT, (conv_minw<KH, BN, TW, EPI, SHP::FIXED>())
       for (int s = 0; s < KS; ++s) {
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
-          const int off = (LIN ? abase[mt][LIN ? dy : 0] + dx * LDP : apix[mt] + toff) + 16 * s + koff;
-          f16x8 ah = *reinterpret_cast<const f16x8*>(lds_hi + off);
-          f16x8 al = *reinterpret_cast<const f16x8*>(lds_lo + off);
-          if constexpr (TW == 1 && KH > 1) {
+          int roff = LIN ? abase[mt][LIN ? dy : 0] + dx * LDP : apix[mt] + toff;
+          if constexpr (ZROW) {
             const int src = trow[mt] + dy - A_PH;
-            if (src < 0 || src >= A_H) {
-              ah = f16x8{};
-              al = f16x8{};
-            }
+            if (src < 0 || src >= A_H) roff = NPIX * LDP;
           }
+          const int off = roff + 16 * s + koff;
+          const f16x8 ah = *reinterpret_cast<const f16x8*>(lds_hi + off);
+          const f16x8 al = *reinterpret_cast<const f16x8*>(lds_lo + off);
 #pragma unroll
           for (int nt = 0; nt < NTL; ++nt) {
             if constexpr (CIL) {   // C^T: rows = channels, columns = pixels
