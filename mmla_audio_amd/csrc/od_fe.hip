@@ -188,25 +188,24 @@ constexpr int P2W = 212;           // power-row pitch (>= 201 + the widest band'
 // pair's own FFT rows: p2(q)[k].c = P[2q + c][k] over the first 1696 B of st[2q], st[2q + 1] (the
 // split reads both frames' Z before it writes the pair's row)
 //
-// A clip is FE_NW waves (one workgroup): wave w runs rounds w, w + NW, ... in its own LDS buffers,
+// A clip is NW waves (one workgroup): wave w runs rounds w, w + NW, ... in its own LDS buffers,
 // the clip max / min are combined through LDS at one barrier, and the epilogue's 16 band blocks
 // are split over the waves.  Finer work units than one wave per clip shorten the tail of a
-// launch whose clip count is not a multiple of the resident clip-waves (config 2: 4096 clips on
-// 256 CUs x 12 waves).
-#ifndef FE_NW
-#define FE_NW 2
-#endif
-constexpr int NW = FE_NW;
+// launch whose clip count is not a multiple of the resident clip-waves (256 CUs x 12 waves): NW 4
+// for small launches (config 2's 4096 clips: 12.8 -> 13.1 M clips/s), NW 2 for large ones (at
+// 65 536 clips NW 4 is 2 % slower than NW 2, which equals NW 1 there) -- A/B, one box.
 struct WaveBuf {
   int16_t win[WIN];                // reflect-padded window of the round, base = 160 f0 - 200
   cf st[R][200];                   // per frame: pass A out [k1][n2] -> Z[k] -> power rows
 };
+template <int NW>
 struct Smem {
   WaveBuf w[NW];
   int zc[NF + 1];                  // ZCR counts of the clip
   uint8_t rb[NF + 1];              // image R byte per column
   float red[2][NW];                // per-wave max / min of the mel power
 };
+constexpr int64_t NW4_MAX_CLIPS = 8192;   // launches up to this size use four waves per clip
 static_assert(sizeof(int16_t) * WIN % 16 == 0, "st must stay 16-B aligned");
 static_assert(sizeof(WaveBuf) % 16 == 0, "wave buffers stay 16-B aligned");
 static_assert(P2W * sizeof(float2) <= 2 * 200 * sizeof(cf), "a pair's power row fits its FFT rows");
@@ -226,12 +225,12 @@ MMLA_DEV void split_power(cf z, cf zr, cf w, float& pk, float& pnk) {
 
 // DB / NM / IMG: which of the dB, normalised and image outputs are written (compile-time, so the
 // epilogue's store counts are static and its waits for the scratch re-reads stay counted)
-template <bool DB, bool NM, bool IMG>
+template <int NW, bool DB, bool NM, bool IMG>
 #ifndef FE_MINB
 #define FE_MINB 3   // waves (= workgroups) per SIMD the register budget is sized for (12.5 KB LDS: 12 per CU)
 #endif
 __global__ void __launch_bounds__(NT * NW, FE_MINB) od_fe_kernel(OdFeArgs a) {
-  __shared__ __attribute__((aligned(16))) Smem sm;
+  __shared__ __attribute__((aligned(16))) Smem<NW> sm;
   const OdFeTables& tb = *a.tables;
   const int lane = threadIdx.x & (NT - 1);
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / NT);
@@ -641,7 +640,7 @@ extern "C" int mmla_debug_fe_times(unsigned long long* host) {
 }
 #endif
 
-size_t od_fe_smem_bytes() { return sizeof(v2::Smem); }
+size_t od_fe_smem_bytes() { return sizeof(v2::Smem<4>); }
 
 bool od_fe_tables_ok(const OdFeTables& t) {
   if (t.mel_taps_lo > v2::T_LO || t.mel_taps_hi > v2::T_HI) return false;
@@ -650,19 +649,25 @@ bool od_fe_tables_ok(const OdFeTables& t) {
   return true;
 }
 
-static void launch_v2(const OdFeArgs& a, int64_t n, hipStream_t s) {
-  const dim3 g((unsigned)n), b(NT * v2::NW);
+template <int NW>
+static void launch_nw(const OdFeArgs& a, int64_t n, hipStream_t s) {
+  const dim3 g((unsigned)n), b(NT * NW);
   const int k = (a.db ? 4 : 0) | (a.norm ? 2 : 0) | (a.img ? 1 : 0);
   switch (k) {
-    case 0: hipLaunchKernelGGL((v2::od_fe_kernel<false, false, false>), g, b, 0, s, a); break;
-    case 1: hipLaunchKernelGGL((v2::od_fe_kernel<false, false, true>), g, b, 0, s, a); break;
-    case 2: hipLaunchKernelGGL((v2::od_fe_kernel<false, true, false>), g, b, 0, s, a); break;
-    case 3: hipLaunchKernelGGL((v2::od_fe_kernel<false, true, true>), g, b, 0, s, a); break;
-    case 4: hipLaunchKernelGGL((v2::od_fe_kernel<true, false, false>), g, b, 0, s, a); break;
-    case 5: hipLaunchKernelGGL((v2::od_fe_kernel<true, false, true>), g, b, 0, s, a); break;
-    case 6: hipLaunchKernelGGL((v2::od_fe_kernel<true, true, false>), g, b, 0, s, a); break;
-    default: hipLaunchKernelGGL((v2::od_fe_kernel<true, true, true>), g, b, 0, s, a); break;
+    case 0: hipLaunchKernelGGL((v2::od_fe_kernel<NW, false, false, false>), g, b, 0, s, a); break;
+    case 1: hipLaunchKernelGGL((v2::od_fe_kernel<NW, false, false, true>), g, b, 0, s, a); break;
+    case 2: hipLaunchKernelGGL((v2::od_fe_kernel<NW, false, true, false>), g, b, 0, s, a); break;
+    case 3: hipLaunchKernelGGL((v2::od_fe_kernel<NW, false, true, true>), g, b, 0, s, a); break;
+    case 4: hipLaunchKernelGGL((v2::od_fe_kernel<NW, true, false, false>), g, b, 0, s, a); break;
+    case 5: hipLaunchKernelGGL((v2::od_fe_kernel<NW, true, false, true>), g, b, 0, s, a); break;
+    case 6: hipLaunchKernelGGL((v2::od_fe_kernel<NW, true, true, false>), g, b, 0, s, a); break;
+    default: hipLaunchKernelGGL((v2::od_fe_kernel<NW, true, true, true>), g, b, 0, s, a); break;
   }
+}
+
+static void launch_v2(const OdFeArgs& a, int64_t n, hipStream_t s) {
+  if (n <= v2::NW4_MAX_CLIPS) launch_nw<4>(a, n, s);
+  else launch_nw<2>(a, n, s);
 }
 
 hipError_t od_fe_launch(const OdFeArgs& a, int64_t n_clips, hipStream_t stream) {
