@@ -59,7 +59,9 @@ def pmc_traffic(workload, stage, clips_per_launch):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
-    ap.add_argument('--steps', type=int, default=3)
+    ap.add_argument('--steps', type=int, default=None,
+                    help='timed steps (default 3; 50 for od_features, whose step is one ~0.3 ms '
+                         'launch, so that host-side jitter stays out of the value)')
     ap.add_argument('--warmup', type=int, default=1)
     ap.add_argument('--workload', default='od_pipeline',
                     choices=['od_pipeline', 'si_pipeline', 'od_features', 'noise_gate'])
@@ -71,7 +73,10 @@ def parse():
     ap.add_argument('--microbatch', type=int, default=0,
                     help='clips per internal micro-batch (0 = the library default)')
     ap.add_argument('--cpu-seconds', type=float, default=20.0)
-    return ap.parse_args()
+    args = ap.parse_args()
+    if args.steps is None:
+        args.steps = 50 if args.workload == 'od_features' else 3
+    return args
 
 
 def launch_ranks(args):

@@ -357,8 +357,9 @@ int take_conv(mmla_ctx* c, Cursor& cur, std::vector<void*>& al, int kh, int kw, 
     w->kpad = (kh * kw * cin + 31) / 32 * 32;
     const size_t n = (size_t)cout * w->kpad;
     std::vector<uint16_t> hi(n), lo(n);
-    // the 3x3 convs feed GEMM 1 (fragment order); conv(4,1) and the 1x1 shortcut keep [co][k] rows
-    resblk_split_weights(k, kh * kw, cin, cout, w->kpad, hi.data(), lo.data(), kh == 3 && kw == 3);
+    // the 3x3 (GEMM 1) and conv(4,1) (GEMM 2) weights in MFMA fragment order; the 1x1 shortcut
+    // keeps [co][k] rows
+    resblk_split_weights(k, kh * kw, cin, cout, w->kpad, hi.data(), lo.data(), kh > 1);
     float* p = nullptr;
     CHK(upload(c, al, hi.data(), n * sizeof(uint16_t), &p));
     w->fh = reinterpret_cast<uint16_t*>(p);

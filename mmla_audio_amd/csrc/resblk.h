@@ -35,6 +35,7 @@ int resblk_k1pad(int cin);
 bool resblk_supported(int cin, int c, bool pool);
 hipError_t resblk_launch(ResBlkArgs a, int cin, int c, bool pool, hipStream_t stream);
 // Host: float32 Keras weights [taps][cin][cout] -> fp16 hi/lo [cout][kpad] with k = tap * cin + ci
-// (zero for k >= taps * cin); frag: GEMM 1's MFMA fragment order [k / 32][cout / 16][64 lanes][8].
+// (zero for k >= taps * cin); frag: the 16x16x32 MFMA B-fragment order [k / 32][cout / 16][64 lanes][8]
+// (GEMM 1's 3x3 and GEMM 2's conv(4,1) weights; the 1x1 shortcut keeps the [cout][kpad] rows).
 void resblk_split_weights(const float* w, int taps, int cin, int cout, int kpad, uint16_t* hi,
                           uint16_t* lo, bool frag);

@@ -24,7 +24,7 @@
 #include "resblk.h"
 
 #ifndef RB_W2LDS
-#define RB_W2LDS 1   // GEMM 2's weights staged in LDS (0: read from L2)
+#define RB_W2LDS 0   // block 1: GEMM 2's weights from L2 in fragment order, 3 workgroups per CU (1: in LDS, 2)
 #endif
 #ifndef RB_EXP
 #define RB_EXP 0   // experiment switch for profiling (0 = product)
@@ -122,11 +122,13 @@ struct Geo {
   static constexpr int KS2 = 4 * C / 32;           // GEMM 2 k-steps
   static constexpr int KSC = (CIN + 31) / 32;      // shortcut (1x1) k-steps
   static constexpr int LW2 = 4 * C + 16;           // halfs per LDS row of GEMM 2's weights (288 B)
-  // GEMM 2's weights live in LDS (B from L2 in GEMM 2 cost more than a third workgroup per CU
-  // bought for the 16-channel block: measured)
-  static constexpr bool W2LDS = RB_W2LDS;
+  // GEMM 2's weights: block 1 reads them from L2 in fragment order, one k-step ahead, so that its
+  // LDS (51 KB) admits a third workgroup per CU: conv 1432 -> 1386 ms per OD step (A/B).  (With
+  // the [co][k] rows and no prefetch the same move had been 7.5 % slower.)  Blocks 2-3 keep them in
+  // LDS: without them they still need 60 KB, two workgroups per CU.
+  static constexpr bool W2LDS = CIN == 16 ? RB_W2LDS : true;
   static constexpr int W2 = W2LDS ? C * LW2 : 0;
-  static constexpr int MINB = 2;                   // resident workgroups per CU (LDS budget)
+  static constexpr int MINB = W2LDS ? 2 : 3;       // resident workgroups per CU (LDS budget)
   static constexpr int PF = 3;                     // GEMM 1 B fragments in flight (k-steps)
   static constexpr int QPP = CIN / 4;              // float4 per halo pixel
   static constexpr int MAXT = (XNP * QPP + NT - 1) / NT;
@@ -269,12 +271,15 @@ __global__ void __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(R
   }
   if constexpr (G::W2LDS) {
   // GEMM 2's weights -> LDS (16-B pieces; rows padded to spread the banks)
+    // (the global copy is in fragment order: k = 8 k8 + e of channel co sits at piece
+    //  ((k / 32) (C / 16) + co / 16) 64 + co % 16 + 16 ((k % 32) / 8))
     for (int i = tid; i < C * (4 * C / 8); i += NT) {
       const int co = i / (4 * C / 8), k8 = i - co * (4 * C / 8);
+      const int src = (((k8 / 4) * (C / 16) + co / 16) * 64 + co % 16 + 16 * (k8 % 4)) * 8;
       *reinterpret_cast<f16x8*>(s_w2h + co * G::LW2 + 8 * k8) =
-          *reinterpret_cast<const f16x8*>(a.w2h + co * 4 * C + 8 * k8);
+          *reinterpret_cast<const f16x8*>(a.w2h + src);
       *reinterpret_cast<f16x8*>(s_w2l + co * G::LW2 + 8 * k8) =
-          *reinterpret_cast<const f16x8*>(a.w2l + co * 4 * C + 8 * k8);
+          *reinterpret_cast<const f16x8*>(a.w2l + src);
     }
   }
 
@@ -509,7 +514,16 @@ __global__ void __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(R
     const _Float16* ahb = smem + (wm * MT2 * TW + col) * TPS;
     const _Float16* alb = ahb + G::TLO;
     const int b2o = ((wn * NTW) * 16 + col) * G::LW2 + 8 * grp;
-    const int b2g = ((wn * NTW) * 16 + col) * 4 * C + 8 * grp;
+    // !W2LDS: GEMM 2's B from L2 in fragment order (resblk_split_weights, frag), one k-step ahead
+    const int b2g = (wn * NTW) * 512 + lane * 8;   // + nt * 512 + s * (C / 16) * 512
+    f16x8 ph[NTW], pl[NTW];
+    if constexpr (!G::W2LDS) {
+#pragma unroll
+      for (int nt = 0; nt < NTW; ++nt) {
+        ph[nt] = *reinterpret_cast<const f16x8*>(a.w2h + b2g + nt * 512);
+        pl[nt] = *reinterpret_cast<const f16x8*>(a.w2l + b2g + nt * 512);
+      }
+    }
 #pragma unroll
     for (int s = 0; s < KS2; ++s) {
       const int kk = 32 * s + 8 * grp;
@@ -522,8 +536,12 @@ __global__ void __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(R
           gh[nt] = *reinterpret_cast<const f16x8*>(s_w2h + b2o + nt * 16 * G::LW2 + 32 * s);
           gl[nt] = *reinterpret_cast<const f16x8*>(s_w2l + b2o + nt * 16 * G::LW2 + 32 * s);
         } else {
-          gh[nt] = *reinterpret_cast<const f16x8*>(a.w2h + b2g + nt * 16 * 4 * C + 32 * s);
-          gl[nt] = *reinterpret_cast<const f16x8*>(a.w2l + b2g + nt * 16 * 4 * C + 32 * s);
+          gh[nt] = ph[nt];
+          gl[nt] = pl[nt];
+          if (s + 1 < KS2) {
+            ph[nt] = *reinterpret_cast<const f16x8*>(a.w2h + b2g + nt * 512 + (s + 1) * (C / 16) * 512);
+            pl[nt] = *reinterpret_cast<const f16x8*>(a.w2l + b2g + nt * 512 + (s + 1) * (C / 16) * 512);
+          }
         }
       }
 #pragma unroll
