@@ -52,7 +52,14 @@ typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 
 constexpr int NT = 256;
 constexpr int TW = 16;
-constexpr int TH = 16;
+constexpr int TH = 16;                 // output rows per tile (block 1; blocks 2-3: TH_NP)
+#ifndef RB_MINB_L2
+#define RB_MINB_L2 3
+#endif
+#ifndef RB_TH2
+#define RB_TH2 16
+#endif
+constexpr int TH_NP = RB_TH2;          // output rows per tile of the non-pool blocks 2-3
 constexpr float ACT_SCALE = 16.0f;     // 2^4: every split activation
 constexpr float W_SCALE = 256.0f;      // 2^8: weights (resblk_split_weights)
 constexpr float UNSCALE = 1.0f / (ACT_SCALE * W_SCALE);
@@ -99,6 +106,7 @@ struct Geo {
                                                    // so every A fragment read feeds C/16 N tiles
   static constexpr int WM = 4 / WN;                // waves along M (tile rows)
   static constexpr int NTW = C / 16 / WN;          // N tiles per wave
+  static constexpr int TH = POOL ? ::TH : TH_NP;   // output rows per tile
   static constexpr int TR = TH + 3;                // t1 rows needed: image rows h0-1 .. h0+TH+1
   static constexpr int TRP = (TR + WM - 1) / WM * WM;   // computed (padded: no per-row branches)
   // input halo rows h0-2 .. h0+TH+2 (the padded t1 row reads one row past it: finite LDS data,
@@ -126,9 +134,9 @@ struct Geo {
   // LDS (51 KB) admits a third workgroup per CU: conv 1432 -> 1386 ms per OD step (A/B).  (With
   // the [co][k] rows and no prefetch the same move had been 7.5 % slower.)  Blocks 2-3 keep them in
   // LDS: without them they still need 60 KB, two workgroups per CU.
-  static constexpr bool W2LDS = CIN == 16 ? RB_W2LDS : true;
+  static constexpr bool W2LDS = CIN == 16 ? RB_W2LDS : TH == 16;
   static constexpr int W2 = W2LDS ? C * LW2 : 0;
-  static constexpr int MINB = W2LDS ? 2 : 3;       // resident workgroups per CU (LDS budget)
+  static constexpr int MINB = W2LDS ? 2 : (TH == 16 ? 3 : RB_MINB_L2);   // resident workgroups per CU
   static constexpr int PF = 3;                     // GEMM 1 B fragments in flight (k-steps)
   static constexpr int QPP = CIN / 4;              // float4 per halo pixel
   static constexpr int MAXT = (XNP * QPP + NT - 1) / NT;
@@ -157,6 +165,7 @@ __global__ void __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(R
   const int clip = blockIdx.x / tiles;
   const int tile = blockIdx.x - clip * tiles;
   const int th_i = tile / a.tiles_w;
+  constexpr int TH = G::TH;
   const int h0 = th_i * TH, w0 = (tile - th_i * a.tiles_w) * TW;
 
   RB_MARK(0);
@@ -671,7 +680,8 @@ bool resblk_supported(int cin, int c, bool pool) {
 hipError_t resblk_launch(ResBlkArgs a, int cin, int c, bool pool, hipStream_t s) {
   if ((int64_t)a.n * a.h * a.w == 0) return hipSuccess;
   if (!resblk_supported(cin, c, pool)) return hipErrorInvalidValue;
-  a.tiles_h = (a.h + TH - 1) / TH;
+  const int th = pool ? TH : TH_NP;
+  a.tiles_h = (a.h + th - 1) / th;
   a.tiles_w = (a.w + TW - 1) / TW;
   if ((int64_t)a.n * a.tiles_h * a.tiles_w > 0x7fffffffLL) return hipErrorInvalidValue;
   if (cin == 16) {
