@@ -132,6 +132,13 @@ int mmla_load_weights(mmla_ctx* ctx, int model_kind, const float* packed, int64_
 int mmla_od_features(mmla_ctx* ctx, const int16_t* pcm, int64_t n_clips, int64_t clip_stride,
                      const int32_t* lens, int32_t clip_len, float* db, float* norm_db, float* zcr,
                      uint8_t* img, uint32_t flags);
+/* Same on float PCM in librosa.load's scale (y = x / 32768 for 16-bit files; any value): the
+ * drop-in's path for what librosa.load(path, sr=None, mono=True) returns from a WAV that is not
+ * 16-bit mono (stereo downmixed by the channel mean, 8/24/32-bit and float files) --
+ * overlap_features_generator.py:72,93.  Zero crossings treat |y| <= 1e-10 as 0, as librosa. */
+int mmla_od_features_f32(mmla_ctx* ctx, const float* y, int64_t n_clips, int64_t clip_stride,
+                         const int32_t* lens, int32_t clip_len, float* db, float* norm_db,
+                         float* zcr, uint8_t* img, uint32_t flags);
 
 /*
  * SpeakerIdentification front-end, replaces input_feature_gen (speaker_identification.py:372-398):

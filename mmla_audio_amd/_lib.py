@@ -47,6 +47,7 @@ SIGNATURES = {
     'mmla_set_precision': [_P, ctypes.c_int],
     'mmla_load_weights': [_P, ctypes.c_int, _P, _I64, _I32, _I32],
     'mmla_od_features': [_P, _P, _I64, _I64, _P, _I32, _P, _P, _P, _P, _U32],
+    'mmla_od_features_f32': [_P, _P, _I64, _I64, _P, _I32, _P, _P, _P, _P, _U32],
     'mmla_si_features': [_P, _P, _I64, _I64, _P, _I32, _P, _P, _U32],
     'mmla_si_features_seq': [_P, _P, _I64, _I64, _P, _U32],
     'mmla_od_forward': [_P, _P, _I64, _P, _U32],
@@ -299,7 +300,15 @@ class Context:
         return a, ln, a.shape[1]
 
     def od_features(self, pcm, lens=None, db=True, norm=True, zcr=True, img=True):
-        a, ln, L = self._pcm(pcm, lens)
+        """int16 PCM [n, L] (or a list of 1-D int16 arrays) -> dict of features.  A float32 array
+        (librosa.load scale) goes through mmla_od_features_f32 instead."""
+        if isinstance(pcm, np.ndarray) and pcm.dtype == np.float32:
+            a = np.ascontiguousarray(pcm)[None] if pcm.ndim == 1 else np.ascontiguousarray(pcm)
+            ln = None if lens is None else np.ascontiguousarray(lens, dtype=np.int32)
+            fn, L = self.lib.mmla_od_features_f32, a.shape[1]
+        else:
+            a, ln, L = self._pcm(pcm, lens)
+            fn = self.lib.mmla_od_features
         n = a.shape[0]
         out = {}
         bufs = {}
@@ -308,7 +317,7 @@ class Context:
                                      ('zcr', zcr, (n, OD_FRAMES), np.float32),
                                      ('img', img, (n, OD_MELS, OD_FRAMES, 3), np.uint8)):
             bufs[key] = np.empty(shape, dt) if want else None
-        self._check(self.lib.mmla_od_features(
+        self._check(fn(
             self.h, _ptr(a), n, a.shape[1], _ptr(ln), L, _ptr(bufs['db']), _ptr(bufs['norm']),
             _ptr(bufs['zcr']), _ptr(bufs['img']), 0), 'mmla_od_features')
         for k, v in bufs.items():

@@ -16,6 +16,7 @@
 #include "nets.h"
 #include "resblk.h"
 #include "od_fe.h"
+#include <type_traits>
 #include "si_fe.h"
 #include "nr.h"
 #include "vad.h"
@@ -417,17 +418,20 @@ void free_allocs(std::vector<void*>& al) {
 
 // ---- PCM staging -------------------------------------------------------------------------------
 
-struct Pcm {
-  const int16_t* p;
+template <typename T>
+struct PcmT {
+  const T* p;
   int64_t stride;
   const int32_t* lens;
   int32_t clip_len;
 };
+using Pcm = PcmT<int16_t>;
 
 // Device view of clips [c0, c0 + cnt): offsets in device mode, a dense copy of the first
 // `need` samples per clip in host mode.
-int stage_pcm(mmla_ctx* c, const int16_t* pcm, int64_t c0, int64_t cnt, int64_t stride,
-              const int32_t* lens, int32_t clip_len, int need, bool dev, Pcm* out) {
+template <typename T>
+int stage_pcm(mmla_ctx* c, const T* pcm, int64_t c0, int64_t cnt, int64_t stride,
+              const int32_t* lens, int32_t clip_len, int need, bool dev, PcmT<T>* out) {
   if (dev) {
     *out = {pcm + c0 * stride, stride, lens ? lens + c0 : nullptr, clip_len};
     return MMLA_OK;
@@ -439,15 +443,15 @@ int stage_pcm(mmla_ctx* c, const int16_t* pcm, int64_t c0, int64_t cnt, int64_t 
     // overlapping windows of one signal (segmentation with step < window): copy the covered span
     // once and let the kernels read window c at c * stride
     const int64_t span = (cnt - 1) * stride + width;
-    CHK(ws_get(c, S_PCM, (size_t)span * sizeof(int16_t), &dp));
-    HIPCHK(c, hipMemcpyAsync(dp, pcm + c0 * stride, span * sizeof(int16_t), hipMemcpyHostToDevice,
+    CHK(ws_get(c, S_PCM, (size_t)span * sizeof(T), &dp));
+    HIPCHK(c, hipMemcpyAsync(dp, pcm + c0 * stride, span * sizeof(T), hipMemcpyHostToDevice,
                              c->stream));
-    *out = {static_cast<int16_t*>(dp), stride, nullptr, (int32_t)std::min<int64_t>(clip_len, width)};
+    *out = {static_cast<T*>(dp), stride, nullptr, (int32_t)std::min<int64_t>(clip_len, width)};
     return MMLA_OK;
   }
-  CHK(ws_get(c, S_PCM, (size_t)cnt * width * sizeof(int16_t), &dp));
-  HIPCHK(c, hipMemcpy2DAsync(dp, width * sizeof(int16_t), pcm + c0 * stride, stride * sizeof(int16_t),
-                             width * sizeof(int16_t), cnt, hipMemcpyHostToDevice, c->stream));
+  CHK(ws_get(c, S_PCM, (size_t)cnt * width * sizeof(T), &dp));
+  HIPCHK(c, hipMemcpy2DAsync(dp, width * sizeof(T), pcm + c0 * stride, stride * sizeof(T),
+                             width * sizeof(T), cnt, hipMemcpyHostToDevice, c->stream));
   int32_t* dl = nullptr;
   if (lens) {
     void* lp = nullptr;
@@ -455,7 +459,7 @@ int stage_pcm(mmla_ctx* c, const int16_t* pcm, int64_t c0, int64_t cnt, int64_t 
     HIPCHK(c, hipMemcpyAsync(lp, lens + c0, cnt * sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
     dl = static_cast<int32_t*>(lp);
   }
-  *out = {static_cast<int16_t*>(dp), width, dl, (int32_t)std::min<int64_t>(clip_len, width)};
+  *out = {static_cast<T*>(dp), width, dl, (int32_t)std::min<int64_t>(clip_len, width)};
   return MMLA_OK;
 }
 
@@ -1224,18 +1228,25 @@ int mmla_load_weights(mmla_ctx* c, int kind, const float* packed, int64_t n_floa
   return fail(c, MMLA_E_INVALID, "unknown model kind %d", kind);
 }
 
-int mmla_od_features(mmla_ctx* c, const int16_t* pcm, int64_t n, int64_t stride,
-                     const int32_t* lens, int32_t clip_len, float* db, float* norm, float* zcr,
-                     uint8_t* img, uint32_t flags) {
+}  // extern "C"
+
+template <typename T>
+static int od_features_common(mmla_ctx* c, const T* pcm, int64_t n, int64_t stride,
+                              const int32_t* lens, int32_t clip_len, float* db, float* norm,
+                              float* zcr, uint8_t* img, uint32_t flags) {
   if (!c) return MMLA_E_INVALID;
-  if (bad_pcm_args(pcm, n, stride, lens, clip_len)) return fail(c, MMLA_E_INVALID, "bad pcm args");
+  if (bad_pcm_args(reinterpret_cast<const int16_t*>(pcm), n, stride, lens, clip_len))
+    return fail(c, MMLA_E_INVALID, "bad pcm args");
+  if (std::is_same<T, float>::value && od_fe_needs_scratch())
+    return fail(c, MMLA_E_INVALID, "float PCM needs the MFMA front-end (unset MMLA_OD_FE_V2)");
   HIPCHK(c, hipSetDevice(c->device));
   const bool dev = flags & MMLA_DEVICE_PTR;
   auto body = [&](int64_t c0, int64_t cnt) -> int {
-    Pcm p;
+    PcmT<T> p;
     CHK(stage_pcm(c, pcm, c0, cnt, stride, lens, clip_len, MMLA_OD_CLIP, dev, &p));
     OdFeArgs a{};
-    a.pcm = p.p;
+    if constexpr (std::is_same<T, float>::value) a.pcm_f32 = p.p;
+    else a.pcm = p.p;
     a.clip_stride = p.stride;
     a.lens = p.lens;
     a.clip_len = p.clip_len;
@@ -1244,9 +1255,11 @@ int mmla_od_features(mmla_ctx* c, const int16_t* pcm, int64_t n, int64_t stride,
     CHK(out_ptr(c, norm, c0 * OD_PIX, cnt * OD_PIX, dev, S_OUT1, &a.norm));
     CHK(out_ptr(c, zcr, c0 * OD_W, cnt * OD_W, dev, S_OUT2, &a.zcr));
     CHK(out_ptr(c, img, c0 * OD_IMG, cnt * OD_IMG, dev, S_OUT3, &a.img));
-    void* ps = nullptr;
-    CHK(ws_get(c, S_FESCR, (size_t)cnt * OD_PIX * sizeof(float), &ps));
-    a.scratch = static_cast<float*>(ps);
+    if (od_fe_needs_scratch()) {   // only the A/B v2 kernel keeps a mel-dB scratch in HBM
+      void* ps = nullptr;
+      CHK(ws_get(c, S_FESCR, (size_t)cnt * OD_PIX * sizeof(float), &ps));
+      a.scratch = static_cast<float*>(ps);
+    }
     LAUNCH(c, MMLA_STAGE_OD_FE, od_fe_bytes(cnt, a), od_fe_launch(a, cnt, c->stream));
     CHK(copy_back(c, db, c0 * OD_PIX, a.db, cnt * OD_PIX, dev));
     CHK(copy_back(c, norm, c0 * OD_PIX, a.norm, cnt * OD_PIX, dev));
@@ -1261,6 +1274,20 @@ int mmla_od_features(mmla_ctx* c, const int16_t* pcm, int64_t n, int64_t stride,
     CHK(for_microbatches(c, true, n, body));
   }
   return finish(c, dev);
+}
+
+extern "C" {
+
+int mmla_od_features(mmla_ctx* c, const int16_t* pcm, int64_t n, int64_t stride,
+                     const int32_t* lens, int32_t clip_len, float* db, float* norm, float* zcr,
+                     uint8_t* img, uint32_t flags) {
+  return od_features_common(c, pcm, n, stride, lens, clip_len, db, norm, zcr, img, flags);
+}
+
+int mmla_od_features_f32(mmla_ctx* c, const float* y, int64_t n, int64_t stride,
+                         const int32_t* lens, int32_t clip_len, float* db, float* norm, float* zcr,
+                         uint8_t* img, uint32_t flags) {
+  return od_features_common(c, y, n, stride, lens, clip_len, db, norm, zcr, img, flags);
 }
 
 int mmla_si_features(mmla_ctx* c, const int16_t* pcm, int64_t n, int64_t stride,
@@ -1416,9 +1443,11 @@ int mmla_od_pipeline(mmla_ctx* c, const int16_t* pcm, int64_t n, int64_t stride,
       a.clip_len = p.clip_len;
       a.tables = c->od_tables;
       a.img = static_cast<uint8_t*>(pimg);
-      void* ps = nullptr;
-      CHK(ws_get(c, S_FESCR, (size_t)cnt * OD_PIX * sizeof(float), &ps));
-      a.scratch = static_cast<float*>(ps);
+      if (od_fe_needs_scratch()) {
+        void* ps = nullptr;
+        CHK(ws_get(c, S_FESCR, (size_t)cnt * OD_PIX * sizeof(float), &ps));
+        a.scratch = static_cast<float*>(ps);
+      }
       LAUNCH(c, MMLA_STAGE_OD_FE, od_fe_bytes(cnt, a), od_fe_launch(a, cnt, c->stream));
       float* dp;
       int32_t* da;
@@ -1514,9 +1543,17 @@ static int vad_run(mmla_ctx* c, const int16_t* pcm, int64_t n, int64_t stride, c
                    uint8_t* speech_out, int32_t max_frames, int16_t* out, int32_t* out_lens,
                    uint32_t flags) {
   if (n < 0 || (n > 0 && (!pcm || !out || !out_lens)) || (!lens && clip_len < 0) ||
-      (n > 1 && stride < (lens ? 1 : clip_len)))
+      (n > 1 && stride < (lens ? 1 : clip_len)) || (n > 0 && lens && stride < 1))
     return fail(c, MMLA_E_INVALID, "bad VAD args");
   if (n == 0) return MMLA_OK;
+  // with lens the row width is the stride: an item longer than its row would read the next item
+  // and its rewrite would run past the output; device-pointer lens are clamped in the
+  // kernels instead
+  if (lens && !(flags & MMLA_DEVICE_PTR))
+    for (int64_t i = 0; i < n; ++i)
+      if (lens[i] > stride)
+        return fail(c, MMLA_E_INVALID, "lens[%lld] = %d exceeds the row width (stride %lld)",
+                    (long long)i, lens[i], (long long)stride);
   const int64_t width = lens ? stride : std::max<int64_t>(clip_len, 1);
   if (max_frames <= 0) max_frames = std::max(1, vad_frames(width));
   if (max_frames > 4096) return fail(c, MMLA_E_INVALID, "more than 4096 frames (2 min) per item");

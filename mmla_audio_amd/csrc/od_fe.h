@@ -16,10 +16,22 @@ struct OdFeTables {
   float tw[20][10][2];      // W200^(k1 * n2)
   float w400k[101][2];      // W400^k, k = 0..100 (even/odd split)
   int mel_taps_lo, mel_taps_hi;   // max non-zeros over bands 0..63 / 64..127
+  // v3 (two-stage matrix DFT on the f16 MFMA, od_fe.hip): the 32x32x16 A fragments of both stages,
+  // fp16 hi / lo bit patterns in fragment order [gemm][k-step][hi, lo][lane][8]
+  //   stage 1, gemm n1 = 0..15:  rows c = 2 k2 + ri, k = n2      (window x DFT-25, x 2^8)
+  //   stage 2, gemm k2' = 0..12: rows 2 i + ri,    k = 2 n1 + ri (twiddle x DFT-16, x 2^8)
+  uint16_t a1[16][2][2][64][8];
+  uint16_t a2[13][2][2][64][8];
+  // v3 mel: band pairs (2 ib, 2 ib + 1) scheduled over the waves of a workgroup with balanced taps:
+  // mel_pair[nw][w * (64 / nw) + k] = k-th pair of wave w when the workgroup has nw waves (4..16)
+  int mel_pair[17][64];
+  int mel_pair_taps[64];    // max non-zeros of the pair's two bands
+  uint16_t zero16;          // a zero sample: the target of reads past a clip's length
 };
 
 struct OdFeArgs {
   const int16_t* pcm;
+  const float* pcm_f32;     // nullable: float PCM (librosa.load scale, y = x / 32768) instead of pcm
   int64_t clip_stride;
   const int32_t* lens;      // nullable
   int32_t clip_len;
@@ -28,10 +40,11 @@ struct OdFeArgs {
   float* norm;              // [n,128,151] nullable
   float* zcr;               // [n,151]     nullable
   uint8_t* img;             // [n,128,151,3] nullable
-  float* scratch;           // [n,151,128] mel-power scratch (frame-major), required
+  float* scratch;           // [n,151,128] mel-power scratch (frame-major): v2 only
 };
 
 void od_fe_build_tables(OdFeTables* t);
 bool od_fe_tables_ok(const OdFeTables& t);   // the mel tap counts fit the kernel's unrolling
 size_t od_fe_smem_bytes();
+bool od_fe_needs_scratch();                  // false for the MFMA kernel (v3, the default)
 hipError_t od_fe_launch(const OdFeArgs& a, int64_t n_clips, hipStream_t stream);

@@ -190,6 +190,7 @@ __global__ void __launch_bounds__(NT_VAD) vad_speech_kernel(VadArgs a) {
   for (int64_t it = st * a.items_per_stream; it < (st + 1) * a.items_per_stream; ++it) {
     int len = a.lens ? a.lens[it] : a.clip_len;
     if (len < 0) len = 0;
+    if (len > a.stride) len = (int)a.stride;   // never past the item's row (device-pointer lens)
     const int nf = min(vad_frames(len), a.max_frames);
     const int16_t* src = a.pcm + it * a.stride;
     uint8_t* flags = a.speech + it * a.max_frames;
@@ -402,6 +403,7 @@ __global__ void __launch_bounds__(NT_COL) vad_collect_kernel(VadArgs a) {
   const int lane = threadIdx.x;
   int len = a.lens ? a.lens[it] : a.clip_len;
   if (len < 0) len = 0;
+  if (len > a.stride) len = (int)a.stride;     // reads and the rewrite stay inside the item's row
   const int nf = min(min(vad_frames(len), a.max_frames), MAXF_LDS);
   const uint8_t* sp = a.speech + it * a.max_frames;
   if (lane == 0) {

@@ -17,15 +17,41 @@ import scipy.io.wavfile as _wavfile
 from . import _lib
 
 
-def _read_wav_int16(path):
-    """librosa.load(path, sr=None) for the reference's 16-bit mono WAVs, kept as int16 PCM
-    (the kernel applies the /32768 scaling)."""
+def _load(path):
+    """``librosa.load(path, sr=None)`` (mono=True; overlap_features_generator.py:72,93) for WAV files.
+
+    librosa 0.8 reads through soundfile as float32 (16-bit x / 2^15, 32- and left-justified 24-bit
+    x / 2^31, unsigned 8-bit (x - 128) / 2^7, float files as stored) and downmixes with the channel
+    mean (``to_mono``: np.mean over channels in float32).  A 16-bit mono file is returned as its
+    int16 samples (the kernel applies / 32768 itself, exactly); anything else as that float32
+    signal, which the float entry point (mmla_od_features_f32) consumes.
+
+    ``sr=None`` keeps the file's rate and the reference then builds its mel basis and FFT framing
+    from it; the HIP front-end is built for 16 kHz only, so any other rate raises ValueError
+    instead of silently computing a 16 kHz spectrogram."""
     sr, x = _wavfile.read(path)
-    if x.ndim > 1:
-        raise ValueError(f'{path}: expected mono audio (the reference records 1 channel)')
-    if x.dtype != np.int16:
-        raise ValueError(f'{path}: expected 16-bit PCM, got {x.dtype}')
-    return sr, x
+    if sr != 16000:
+        raise ValueError(f'{path}: sample rate {sr} Hz; the HIP front-end computes the reference\'s '
+                         'features at 16 kHz only (librosa.load(sr=None) keeps the file rate)')
+    if x.dtype == np.int16 and x.ndim == 1:
+        return sr, x
+    if x.dtype == np.int16:
+        y = x.astype(np.float32) / np.float32(32768.0)
+    elif x.dtype == np.int32:
+        y = x.astype(np.float32) * np.float32(2.0 ** -31)
+    elif x.dtype == np.uint8:
+        y = (x.astype(np.float32) - np.float32(128.0)) * np.float32(1.0 / 128.0)
+    elif x.dtype in (np.float32, np.float64):
+        y = x.astype(np.float32)
+    else:
+        raise ValueError(f'{path}: unsupported WAV sample type {x.dtype}')
+    if y.ndim > 1:
+        y = np.mean(y.T, axis=0)          # librosa.to_mono on [channels, n]
+    return sr, np.ascontiguousarray(y, dtype=np.float32)
+
+
+def _features(ctx, x, **kw):
+    return ctx.od_features(x[None], lens=np.array([len(x)], np.int32), **kw)
 
 
 def write_png_rgba(path, rgb):
@@ -90,15 +116,14 @@ class OverlapFeaturesGenerator:
         """-> (s_db float32 [128,151], s_db_norm float32 [128,151])  (:65-85)."""
         if n_mels != 128:
             raise ValueError('n_mels must be 128 (the kernel is built for the reference default)')
-        _, x = _read_wav_int16(wav_file_path)
-        f = self._ctx.od_features(x[None], lens=np.array([len(x)], np.int32), zcr=False, img=False)
+        _, x = _load(wav_file_path)
+        f = _features(self._ctx, x, zcr=False, img=False)
         return f['db'][0], f['norm'][0]
 
     def generate_zcr(self, wav_file_path):
         """-> float64 [1, 151] zero-crossing rate (:87-101)."""
-        _, x = _read_wav_int16(wav_file_path)
-        f = self._ctx.od_features(x[None], lens=np.array([len(x)], np.int32), db=False,
-                                  norm=False, img=False)
+        _, x = _load(wav_file_path)
+        f = _features(self._ctx, x, db=False, norm=False, img=False)
         return self._zcr64(f['zcr'][0])[None]
 
     @staticmethod
@@ -121,8 +146,8 @@ class OverlapFeaturesGenerator:
         otherwise writes ``out_dir + out_name`` as the PNG the reference's plt.imsave writes."""
         if not os.path.isdir(out_dir):
             os.mkdir(out_dir)
-        _, x = _read_wav_int16(wav_file_path)
-        f = self._ctx.od_features(x[None], lens=np.array([len(x)], np.int32), db=False)
+        _, x = _load(wav_file_path)
+        f = _features(self._ctx, x, db=False)
         if out_name is None:
             img = np.empty((128, 151, 3), np.float64)
             img[..., 0] = self._zcr64(f['zcr'][0])[None, :]

@@ -32,8 +32,12 @@ N_BINS = 1 + N_FFT // 2          # 201
 
 
 def load_int16(pcm):
-    """librosa.load(path, sr=None) on a 16-bit mono WAV: soundfile float32 = x / 32768."""
-    return (np.asarray(pcm, dtype=np.int16).astype(np.float32) / np.float32(32768.0)).astype(np.float32)
+    """librosa.load(path, sr=None) on a 16-bit mono WAV: soundfile float32 = x / 32768.  A float32
+    array is taken as librosa.load's output already (any other WAV format, stereo downmixed)."""
+    pcm = np.asarray(pcm)
+    if pcm.dtype == np.float32:
+        return pcm
+    return (pcm.astype(np.int16).astype(np.float32) / np.float32(32768.0)).astype(np.float32)
 
 
 def pad_trunc(y, n=CLIP):

@@ -135,3 +135,59 @@ def test_load_model_requires_trained_weights(tmp_path):
     with pytest.warns(UserWarning):
         m = models.load_model(str(d), allow_synthetic=True)
     assert m.synthetic and m.predict(np.zeros((1, 128, 151, 3), np.float32)).shape == (1, 2)
+
+
+def _librosa_load_ref(x):
+    """librosa.load(sr=None, mono=True) of the WAV data x that scipy reads back: soundfile float32
+    conversion, then to_mono (np.mean over channels in float32) -- librosa 0.8 util/audio."""
+    if x.dtype == np.int16:
+        y = x.astype(np.float32) / np.float32(32768.0)
+    elif x.dtype == np.int32:
+        y = x.astype(np.float32) * np.float32(2.0 ** -31)
+    elif x.dtype == np.uint8:
+        y = (x.astype(np.float32) - np.float32(128.0)) * np.float32(1.0 / 128.0)
+    else:
+        y = x.astype(np.float32)
+    return np.mean(y.T, axis=0) if y.ndim > 1 else y
+
+
+@pytest.mark.parametrize('kind', ['stereo_int16', 'float32', 'int32', 'uint8'])
+def test_generate_mels_librosa_load_formats(tmp_path, kind):
+    """the drop-in reads WAVs the way librosa.load(path, sr=None) does
+    (overlap_features_generator.py:72,93): stereo is downmixed by the channel mean, 8/32-bit and
+    float files are scaled as soundfile does; checked against the oracle on that float signal."""
+    from oracle import od_fe, synth
+    from mmla_audio_amd.overlap_features_generator import OverlapFeaturesGenerator
+    a, b = synth.clip(0, 30000), synth.clip(1, 30000)
+    if kind == 'stereo_int16':
+        data = np.stack([a, b], axis=1)
+    elif kind == 'float32':
+        data = (a.astype(np.float32) / 32768.0 * 0.9).astype(np.float32)
+    elif kind == 'int32':
+        data = a.astype(np.int32) * 65536 + 12345
+    else:
+        data = (a.astype(np.int32) // 256 + 128).astype(np.uint8)
+    p = str(tmp_path / f'{kind}.wav')
+    wavfile.write(p, 16000, data)
+    _, back = wavfile.read(p)
+    y = _librosa_load_ref(back)
+    ofg = OverlapFeaturesGenerator(wl=25, hl=10)
+    s_db, norm = ofg.generate_mels(p)
+    ref = od_fe.od_features(y)
+    assert np.abs(norm - ref['norm']).max() <= 1e-4, kind
+    assert np.abs(s_db - ref['db']).max() <= 5e-3, kind
+    assert np.array_equal(ofg.generate_zcr(p), ref['zcr']), kind
+    got = ofg.generate_zcr_image(p, str(tmp_path) + '/', None)
+    assert np.abs(got - ref['image']).max() <= 1e-4
+
+
+def test_generate_mels_rejects_other_rates(tmp_path):
+    """sr=None keeps the file's rate; the reference would build a 22.05 kHz mel basis.  The HIP
+    front-end is 16 kHz only, so the drop-in raises instead of computing a 16 kHz spectrogram."""
+    from mmla_audio_amd.overlap_features_generator import OverlapFeaturesGenerator
+    p = str(tmp_path / 'r22k.wav')
+    wavfile.write(p, 22050, np.zeros(30000, np.int16))
+    ofg = OverlapFeaturesGenerator(wl=25, hl=10)
+    for fn in (ofg.generate_mels, ofg.generate_zcr):
+        with pytest.raises(ValueError, match='16 kHz'):
+            fn(p)

@@ -70,6 +70,41 @@ def test_independent_streams(ctx):
             assert np.array_equal(flags[2 * s + k], f) and np.array_equal(out[2 * s + k], o), (s, k)
 
 
+def test_lens_longer_than_row_rejected_or_clamped(ctx):
+    """an item length above the row width (the stride) must not read the next item or
+    write past the output.  Host call: MMLA_E_INVALID.  Device-pointer call (lens not visible to the
+    host): the kernels clamp to the row, so the output stays inside its rows and the guard words
+    behind the last row are untouched."""
+    import torch
+    from mmla_audio_amd import _lib
+    x = np.stack([_clip(40), _clip(41)])
+    ctx.vad_reset(2, 3)
+    with pytest.raises(_lib.MmlaError):
+        ctx.vad_remove_silence(x, lens=np.array([x.shape[1], x.shape[1] + 480], np.int32))
+
+    n, L = x.shape
+    dev = torch.device('cuda:0')
+    pcm = torch.from_numpy(x).to(dev)
+    lens = torch.tensor([L, 3 * L], dtype=torch.int32, device=dev)
+    guard = 4096
+    out = torch.full((n * L + guard,), 12345, dtype=torch.int16, device=dev)
+    olen = torch.zeros(n, dtype=torch.int32, device=dev)
+    nf = (L - 1) // 480
+    speech = torch.zeros((n, nf), dtype=torch.uint8, device=dev)
+    ctx.vad_reset(2, 3)
+    rc = ctx.lib.mmla_vad_remove_silence(ctx.h, pcm.data_ptr(), n, L, lens.data_ptr(), L, 1,
+                                         out.data_ptr(), olen.data_ptr(), speech.data_ptr(), nf,
+                                         _lib.MMLA_DEVICE_PTR)
+    torch.cuda.synchronize()
+    assert rc == 0
+    assert bool((out[n * L:] == 12345).all()), 'write past the last row'
+    assert int(olen.max()) <= L
+    # the clamped item (its own stream, fresh detector) equals the item at its true length
+    o, _ = ovad.remove_silence(x[1], webrtc_vad.Vad(3).is_speech)
+    got = out[L:L + int(olen[1])].cpu().numpy()
+    assert np.array_equal(got, o)
+
+
 def test_state_persists_across_calls(ctx):
     a, b = _clip(30), _clip(31)
     ctx.vad_reset(1, 3)
