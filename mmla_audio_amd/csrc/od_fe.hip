@@ -663,6 +663,9 @@ typedef uint16_t us2 __attribute__((ext_vector_type(2)));
 #ifndef FE3_NWV
 #define FE3_NWV 16
 #endif
+#ifndef FE3_SKIP
+#define FE3_SKIP 0   // dev timing builds only: 1 staging, 2 stage 1, 4 stage 2, 8 mel, 16 norm stores skipped
+#endif
 constexpr int NWV = FE3_NWV;                  // waves per workgroup (one workgroup per CU)
 constexpr int NTH = 64 * NWV;
 constexpr int TF = 32;                        // frames per tile = the MFMA's 32 columns
@@ -692,7 +695,7 @@ struct Smem {
   _Float16 z_hi[13 * TF * ZP], z_lo[13 * TF * ZP];   // stage-1 output; image epilogue [64][151] f32 over both
   float p[(PROWS + 1) * PP + 64];             // power [bin][frame] (+ the trash row)
   uint32_t ztrash[128];                       // stage 1's one unused (k2 = 14) word per lane, hi / lo
-  float mw[128 * MW];                         // mel taps [band][j] (zero past the band's non-zeros)
+  alignas(16) float mw[128 * MW];             // mel taps [band][j] (zero past the band's non-zeros)
   int mst[128];                               // first bin of each band
   uint8_t sgn[NCH + 16];                      // per chunk: sign bits of its 8 samples
   uint8_t cnt[NCH + 16];                      // per chunk: crossings (low 4 bits), one into its first sample (bit 4)
@@ -844,7 +847,7 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
         for (int k = 0; k < PPW; ++k) dbv[u][k] = dbv[u + 1][k];
       // ---- stage the tile: chunk c holds p = 8c .. 8c + 7 (reflect-padded, zero past len), split
       //      x' = x 2^-12 into fp16 hi + lo, transposed store T[p & 15][p >> 4] = (hi, lo) ------
-      {
+      if constexpr (!(FE3_SKIP & 1)) {
         const int c = tid - (t == NTILE - 1 ? ROT4 : 0);
         const int i0 = ibase + 8 * c;
         const bool live = c >= 0 && c < NCH;
@@ -954,7 +957,7 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
       }
 
       // ---- stage 1 (wave = n1 G1 wid .. + G1 - 1): D1 = A1[n1] (32 x 32) . B1 (32 n2 x 32 frames) ----
-      {
+      if constexpr (!(FE3_SKIP & 2)) {
         f32x16 acc[G1];
 #pragma unroll
         for (int g = 0; g < G1; ++g) {
@@ -1033,7 +1036,7 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
 #pragma unroll
       for (int j = 0; j < G2; ++j) {
         const int k2 = wid + NWV * j;
-        if (k2 >= 13) continue;
+        if (k2 >= 13 || (FE3_SKIP & 4)) continue;
         const _Float16* zh = sm.z_hi + (k2 * TF + r) * ZP + 8 * hh;
         const _Float16* zl = sm.z_lo + (k2 * TF + r) * ZP + 8 * hh;
         f32x16 acc = {};
@@ -1085,6 +1088,7 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
       //      count is wave-uniform, taps past a band's own count are zero weights) -> 10 log10 S ----
 #pragma unroll
       for (int k = 0; k < PPW; ++k) {
+        if (FE3_SKIP & 8) break;
         const int b = 2 * pair[k] + hh;
         const float* wp = sm.mw + b * MW;
         const float* pp = sm.p + sm.mst[b] * PP + r;
@@ -1148,7 +1152,7 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
             const float d = fmaxf(dbv[t][k] - ref_db, thr);
             // (d - min) / (max - min) as a multiply by the reciprocal (<= 2 ulp; as v2); 0 * inf =
             // NaN keeps the digital-silence NaN
-            if (NM) a.norm[ob + b * NF + f] = (d - d_min) * inv_diff;
+            if (NM && !(FE3_SKIP & 16)) a.norm[ob + b * NF + f] = (d - d_min) * inv_diff;
             if (DB) a.db[ob + b * NF + f] = d;
           }
         }

@@ -63,12 +63,16 @@ def silent_segments(segments, ctx=None, vad_mode=3, reset=True, speech=None):
 
 
 def post_analyse_conversation(whole_pcm, segments, model, speaker_id_dict, ctx=None, vad_mode=3,
-                              speech=None):
+                              speech=None, reset_vad=False):
     """-> (labels per 256-frame window: speaker name or 'silent', probabilities [S, K], silent
     segment indices).  ``model`` is a SpeakerIdModel (models.load_model) or anything with
-    ``predict([S, 256, 39])``; `speech` as in silent_segments."""
+    ``predict([S, 256, 39])``; `speech` as in silent_segments.
+
+    The reference keeps ONE module-level ``webrtcvad.Vad(3)`` (:26) for every conversation of
+    post_analysing, so its adaptive state carries from one conversation to the next: the context's
+    detector is created on the first call and kept by later ones (``reset_vad=True`` starts afresh)."""
     ctx = ctx or getattr(model, 'ctx', None) or _lib.default_context()
-    silent, _ = silent_segments(segments, ctx, vad_mode, speech=speech)
+    silent, _ = silent_segments(segments, ctx, vad_mode, reset=reset_vad, speech=speech)
     test_x = conversation_features(np.asarray(whole_pcm, np.int16))
     results = model.predict(test_x)
     labels = []

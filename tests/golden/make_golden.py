@@ -386,7 +386,140 @@ def _sipost_case(si_mod, tmp):
             'segment_len': np.array(40960), 'n_segments': np.array(len(loud))}
 
 
-def main(parts=('od', 'si', 'seg', 'exp', 'vad', 'sipost')):
+ODPOST_CONVS = [
+    # (file under whole/, seeds of its 2.5 s voiced pieces, samples): audio* -> 3 noise-gate passes,
+    # zoom* -> none (overlap_detection_post_processing.py:182-190)
+    ('audio_conv0.wav', (40, 41, 42), 84800),
+    ('zoom_conv1.wav', (43, 44), 64000),
+]
+
+
+def _pcm16_rule(y):
+    """sf.write(..., PCM_16) as mmla_pcm16 restates libsndfile: (short) lrintf(32767 * y)"""
+    y = np.asarray(y, dtype=np.float32)
+    return (np.rint(np.float32(32767.0) * y).astype(np.int64) & 0xFFFF).astype(np.uint16).view(np.int16)
+
+
+def _odpost_case(ofg_mod, tmp):
+    """post_anlysing (overlap_detection_post_processing.py:151-226) on two synthetic conversations.
+
+    Stubs: librosa.load -> soundfile's float32 read (no resampling: the one call with the default
+    22.05 kHz only feeds the peak-normalised file that the pydub export overwrites, :103-123);
+    soundfile.write -> PCM_16 by the libsndfile rule; pydub AudioSegment -> WAV read / export (the
+    call passes dbfs=0, falsy, so no gain); noisereduce -> oracle/noisereduce.py; the Keras model ->
+    the float64 oracle OD-NET with the seed-0 synthetic weights; tf.io / decode_png -> PIL.  The two
+    Windows path separators of the source (:32 and :182/:185) are replaced by os.sep before it is
+    compiled, so that it runs on Linux; nothing else of the reference text changes."""
+    import datetime as _dt
+    import scipy.io.wavfile as wavfile
+    from oracle import nets, noisereduce as onr
+    from mmla_audio_amd import weights
+
+    def load(path, sr=22050):
+        rate, x = wavfile.read(path)
+        y = x.astype(np.float32) / np.float32(32768.0)
+        return y, (rate if sr is None else sr)
+
+    sys.modules['librosa'].load = load
+
+    def sf_write(path, y, sr, format=None):
+        wavfile.write(path, int(sr), _pcm16_rule(y))
+
+    _module('soundfile', write=sf_write)
+
+    class AudioSegment:
+        def __init__(self, pcm, rate):
+            self.pcm, self.rate = pcm, rate
+
+        @classmethod
+        def from_file(cls, path, format=None):
+            rate, x = wavfile.read(path)
+            assert x.dtype == np.int16 and x.ndim == 1
+            return cls(x, rate)
+
+        def set_frame_rate(self, rate):
+            assert rate == self.rate, 'synthetic conversations are 16 kHz'
+            return self
+
+        @property
+        def dBFS(self):
+            raise AssertionError('post_anlysing passes dbfs=0: no gain step')
+
+        def export(self, path, format=None):
+            wavfile.write(path, self.rate, self.pcm)
+
+    _module('pydub', AudioSegment=AudioSegment)
+    def reduce_noise(y_noise, y, sr, stationary):
+        assert stationary
+        return onr.reduce_noise(y, sr, y_noise)
+
+    _module('noisereduce', reduce_noise=reduce_noise)
+    _module('webrtcvad', Vad=_Anything)
+    _module('overlap_degree_distribution')
+    sys.modules['overlap_features_generator'] = ofg_mod
+    W = weights.synthetic(weights.OD, seed=0)
+
+    class StubModel:
+        def predict(self, x):
+            return nets.od_forward(np.asarray(x, np.float64), W)
+
+    tf = sys.modules['tensorflow']
+    tf.keras.models.load_model = lambda path: StubModel()
+    tf.io = types.SimpleNamespace(read_file=lambda path: path)
+    tf.image = types.SimpleNamespace(decode_png=lambda path, ch: _png_rgb(path))
+    tf.stack = lambda xs, axis=0: types.SimpleNamespace(numpy=lambda: np.stack(xs, axis=axis))
+
+    path = os.path.join(REF, 'OverlapDetection/scripts/overlap_detection_post_processing.py')
+    src = open(path).read()
+    assert src.count('src_dir + "\\\\" + f') == 1 and src.count("onewav.split('\\\\')") == 2
+    src = src.replace('src_dir + "\\\\" + f', 'src_dir + os.sep + f').replace(
+        "onewav.split('\\\\')", 'onewav.split(os.sep)')
+    post = types.ModuleType('ref_od_post')
+    post.__file__ = path
+    exec(compile(src, path, 'exec', dont_inherit=True), post.__dict__)
+
+    root = os.path.join(tmp, 'odpost')
+    pt = os.path.join(root, 'experiment', 'recordings', 'post-time')
+    for d in ('whole', 'standardized', 'segments', 'features'):
+        os.makedirs(os.path.join(pt, d), exist_ok=True)
+    os.makedirs(os.path.join(root, 'experiment', 'logs'), exist_ok=True)
+    post.Root_Dir = root
+    post.NOISE_PATH = os.path.join(root, 'experiment/Ambient_Noise.wav')
+    rng = np.random.default_rng(404)
+    noise = (rng.standard_normal(32000) * 300).astype(np.int16)
+    _write_wav(post.NOISE_PATH, noise)
+    out = {'noise': noise, 'names': np.array([c[0] for c in ODPOST_CONVS])}
+    for i, (name, seeds, n) in enumerate(ODPOST_CONVS):
+        pieces = [synth.clip(sd, 40000).astype(np.float64) * 0.5 for sd in seeds]
+        x = np.concatenate(pieces)[:n] + rng.standard_normal(n) * 300
+        x = np.clip(np.round(x), -32768, 32767).astype(np.int16)
+        _write_wav(os.path.join(pt, 'whole', name), x)
+        out[f'pcm_{i}'] = x
+
+    class FixedClock(_dt.datetime):
+        @classmethod
+        def today(cls):
+            return _dt.datetime(2026, 10, 17, 9, 30, 0)
+
+    post.datetime = FixedClock
+    post.post_anlysing()
+    for i, (name, _, _) in enumerate(ODPOST_CONVS):
+        stem = name[:-4]
+        _, std = wavfile.read(os.path.join(pt, 'standardized', name))
+        listing = os.listdir(os.path.join(pt, 'segments', stem))
+        log = open(os.path.join(root, 'experiment', 'logs', stem + '.txt')).read()
+        rows = log.strip().split('\n')[1:]
+        labels = {listing[int(r.split('\t')[0])]: r.split('\t')[1] for r in rows}
+        out[f'std_{i}'] = std
+        out[f'log_{i}'] = np.array(log)
+        out[f'listing_{i}'] = np.array(listing)
+        out[f'seg_names_{i}'] = np.array(sorted(labels, key=lambda f: int(f.split('_')[-3])))
+        out[f'seg_labels_{i}'] = np.array([labels[f] for f in out[f'seg_names_{i}']])
+        print('ODPOST', name, len(std), 'samples,', len(listing), 'segments:', list(out[f'seg_labels_{i}']))
+    return out
+
+
+def main(parts=('od', 'si', 'seg', 'exp', 'vad', 'sipost', 'odpost')):
     _install_stubs()
     ofg_mod = _load_reference('OverlapDetection/scripts/overlap_features_generator.py', 'ref_ofg')
     si_mod = _load_reference('SpeakerIdentification/scripts/speaker_identification.py', 'ref_si')
@@ -394,6 +527,10 @@ def main(parts=('od', 'si', 'seg', 'exp', 'vad', 'sipost')):
     assert ofg.get_attributes() == (400, 160, 16000)
 
     tmp = tempfile.mkdtemp(prefix='mmla_golden_')
+    if 'odpost' in parts:
+        np.savez_compressed(os.path.join(HERE, 'odpost_golden.npz'), **_odpost_case(ofg_mod, tmp))
+        if parts == ('odpost',):
+            return
     if 'vad' in parts:
         np.savez_compressed(os.path.join(HERE, 'vad_golden.npz'), **_vad_cases(tmp))
     if 'sipost' in parts:
@@ -446,4 +583,4 @@ def main(parts=('od', 'si', 'seg', 'exp', 'vad', 'sipost')):
 
 
 if __name__ == '__main__':
-    main(tuple(sys.argv[1:]) or ('od', 'si', 'seg', 'exp', 'vad', 'sipost'))
+    main(tuple(sys.argv[1:]) or ('od', 'si', 'seg', 'exp', 'vad', 'sipost', 'odpost'))

@@ -43,3 +43,60 @@ def test_strided_host_path_bounds(model):
     sig = synth.clip(70, 30000)
     with pytest.raises(_lib.MmlaError):
         model.ctx.od_pipeline_strided(sig, 3, 8000, 24000)     # last window runs past the end
+
+
+def test_post_anlysing_chain_matches_reference(tmp_path):
+    """the OD offline chain (overlap_detection_post_processing.py:151-226) --
+    standardise (3 stationary noise-gate passes + PCM_16 rewrites for audio*, none for zoom*),
+    1.5 s segmentation, one fused features + OD-NET call per conversation, TSV log -- against the
+    reference's own post_anlysing run with stubs (tests/golden/odpost_golden.npz, make_golden.py
+    'odpost'; the float64 oracle OD-NET with the seed-0 synthetic weights stands in for Keras).
+    The standardised PCM agrees to the noise gate's rounding ties; the log lists segments in this directory's os.listdir order, so it is rebuilt from the reference's
+    per-segment labels in that order."""
+    import datetime
+    import os
+    import scipy.io.wavfile as wavfile
+    from mmla_audio_amd import models, weights, overlap_detection_post_processing as odpp
+    g = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden', 'odpost_golden.npz'))
+    root = str(tmp_path)
+    pt = os.path.join(root, 'experiment', 'recordings', 'post-time')
+    for d in ('whole', 'standardized', 'segments', 'features'):
+        os.makedirs(os.path.join(pt, d))
+    os.makedirs(os.path.join(root, 'experiment', 'logs'))
+    wavfile.write(os.path.join(root, 'experiment', 'Ambient_Noise.wav'), 16000, g['noise'])
+    names = list(g['names'])
+    for i, name in enumerate(names):
+        wavfile.write(os.path.join(pt, 'whole', name), 16000, g[f'pcm_{i}'])
+    model = models.OverlapDetectionModel(weights.synthetic(weights.OD, seed=0))
+    t0 = datetime.datetime(2026, 10, 17, 9, 30, 0)
+    out = odpp.post_anlysing(root, model, start_time=t0)
+    for i, name in enumerate(names):
+        stem = name[:-4]
+        _, std = wavfile.read(os.path.join(pt, 'standardized', name))
+        # nr.hip equals the restated gate to ~1e-7 of the peak on 99.9 % of the samples, with rare
+        # mask-threshold flips (test_gpu_vad.py::test_save_wave_file_chain bounds: 1e-5 / 2e-2)
+        d = np.abs(std.astype(np.int64) - g[f'std_{i}'].astype(np.int64))
+        assert std.shape == g[f'std_{i}'].shape and np.mean(d > 0) <= 1e-3, name
+        assert np.quantile(d, 0.999) <= 1 and d.max() <= 0.02 * 32767, name
+        want = dict(zip(g[f'seg_names_{i}'], g[f'seg_labels_{i}']))
+        listing = os.listdir(os.path.join(pt, 'segments', stem))
+        assert sorted(listing) == sorted(want)
+        assert dict(out[name]) == want, name
+        lines = ['segment\toverlapped degree\ttimestamp']
+        for count, f in enumerate(listing):
+            lines.append(f'{count}\t{want[f]}\t{t0 + datetime.timedelta(seconds=1.5 * count)}')
+        log = open(os.path.join(root, 'experiment', 'logs', stem + '.txt')).read()
+        assert log == '\n'.join(lines) + '\n'
+        if list(listing) == list(g[f'listing_{i}']):       # same directory order: the very bytes
+            assert log == str(g[f'log_{i}'])
+
+
+def test_offline_labels_map_silent_windows(model):
+    """a window shorter than 4000 samples comes back as argmax -1; the labels and the
+    log map it to 'silent' (record_on_pc.py:141-154) instead of raising KeyError."""
+    from mmla_audio_amd import overlap_detection_post_processing as odpp
+    sig = synth.clip(71, 3000)
+    model._ensure_loaded()
+    probs, am = model.ctx.od_pipeline_strided(sig, 1, 3000, 3000)
+    assert int(am[0]) == -1
+    assert odpp.LABELS[str(int(am[0]))] == 'silent'

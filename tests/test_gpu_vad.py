@@ -191,3 +191,35 @@ def test_si_post_analysing_flow(tmp_path, ctx):
     # the real detector on the same conversation runs and yields a subset of silent segments
     labels2, _, silent2 = sp.post_analyse_conversation(whole, segments, StubModel(), spk, ctx=ctx)
     assert len(labels2) == len(labels) and all(0 <= i < n_seg for i in silent2)
+
+
+def test_si_post_detector_state_carries_across_conversations(ctx):
+    """the reference's module-level Vad(3) (speaker_identification_post_processing.py:26)
+    keeps its adaptive state from one conversation to the next; post_analyse_conversation keeps the
+    context's detector after its first call.  Checked against ONE oracle detector run over both
+    conversations' segments in order."""
+    from mmla_audio_amd import speaker_identification_post_processing as sp
+
+    class StubModel:
+        def predict(self, x):
+            return np.full((len(x), 2), 0.5)
+
+    convs = [[_clip(60 + 2 * c + k, 40960) for k in range(2)] for c in range(2)]
+    ref = webrtc_vad.Vad(3)
+    want = [[i for i, s in enumerate(segs) if len(ovad.remove_silence(s, ref.is_speech)[0]) < 4000]
+            for segs in convs]
+    got = []
+    for c, segs in enumerate(convs):
+        _, _, silent = sp.post_analyse_conversation(np.concatenate(segs), segs, StubModel(),
+                                                    {'0': 'a', '1': 'b'}, ctx=ctx, reset_vad=(c == 0))
+        got.append(list(silent))
+    assert got == want
+    # the carried state matters on this input: a fresh detector on the second conversation decides
+    # at least one frame differently than the one that saw the first conversation
+    ref_c = webrtc_vad.Vad(3)
+    for s_ in convs[0]:
+        ovad.remove_silence(s_, ref_c.is_speech)
+    carried = [ovad.remove_silence(s_, ref_c.is_speech)[1] for s_ in convs[1]]
+    fresh = webrtc_vad.Vad(3)
+    alone = [ovad.remove_silence(s_, fresh.is_speech)[1] for s_ in convs[1]]
+    assert any(not np.array_equal(a, b) for a, b in zip(carried, alone))
