@@ -39,6 +39,8 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
+#include <utility>
 
 #ifndef FE_EXP
 #define FE_EXP 0   // 1: per-phase s_memtime totals of the first 4096 clips (tools/fe_timeline.py)
@@ -650,7 +652,8 @@ __global__ void __launch_bounds__(NT * NW, FE_MINB) od_fe_kernel(OdFeArgs a) {
 //   power |X|^2 -> P[bin][f] (LDS) -> sparse Slaney mel on the VALU (lane = band m and m + 64, as v2)
 //
 // Arithmetic: error-compensated 3xFP16 with f32 accumulation (x' = x 2^-12 splits int16 exactly into
-// fp16 hi + lo; A1, A2 x 2^8 so their lo halves stay normal; Y = stage-1 output split hi/lo before
+// fp16 hi + lo; A1 x 2^9, A2 x 2^7 so their lo halves stay normal (Z = 2 Y: |Z| < 51200, lo normal
+// for |Y| > 2^-4); Z = stage-1 output split hi/lo before
 // stage 2): acc += lo(a) hi(b) + hi(a) lo(b) + hi(a) hi(b).  The numpy model of this dataflow
 // (tools/fe_mfma_model.py) is exact to 3.5e-15 in float64 and, in fp16/f32, flips 2.8e-5 of the image
 // pixels against the float64 oracle (an fp32 FFT: ~8e-5).
@@ -686,27 +689,47 @@ constexpr int ROT4 = 9;                       // tile 4: chunk c is staged by th
 static_assert(NCH + ROT4 <= NTH, "one staged chunk per thread");
 static_assert(G1 == 1, "stage 1: one GEMM per wave (16 waves)");
 constexpr float X_SCALE = 1.0f / 4096.0f;     // x' = x 2^-12
-constexpr float Y_SCALE = 2.0f;               // Z = 2 Y before the split (|2Y| < 51200; lo normal for |Y| > 2^-4)
-constexpr float P_SCALE = 0x1p-38f;           // |X_ref|^2 = |D2|^2 2^-38 (x' 2^-12, A1 2^8, Z 2^1, A2 2^7, y = x 2^-15)
+constexpr float P_SCALE = 0x1p-38f;           // |X_ref|^2 = |D2|^2 2^-38 (x' 2^-12, A1 2^9, A2 2^7, y = x 2^-15),
+                                              //   folded into the mel weights (power-of-two: exact)
 static_assert(16 % NWV == 0 && 64 % NWV == 0, "work split over the waves");
 
 struct Smem {
-  uint32_t t[16 * TP];                        // staged samples, transposed: (hi, lo) fp16 pair of x'[16 q + n1]
-  _Float16 z_hi[13 * TF * ZP], z_lo[13 * TF * ZP];   // stage-1 output; image epilogue [64][151] f32 over both
+  // the buffers read at lane-dependent addresses plus constant offsets first: their offsets stay
+  // below 64 KB, the ds instructions' immediate field (else a VALU add per read)
   float p[(PROWS + 1) * PP + 64];             // power [bin][frame] (+ the trash row)
+  alignas(16) float mw[128 * MW];             // mel taps [band][j] x P_SCALE (zero past the band's non-zeros)
+  int mst[128];                               // first bin of each band x PP (its P row offset)
   uint32_t ztrash[128];                       // stage 1's one unused (k2 = 14) word per lane, hi / lo
-  alignas(16) float mw[128 * MW];             // mel taps [band][j] (zero past the band's non-zeros)
-  int mst[128];                               // first bin of each band
+  uint32_t t[16 * TP];                        // staged samples, transposed: (hi, lo) fp16 pair of x'[16 q + n1]
+  _Float16 z_hi[13 * TF * ZP], z_lo[13 * TF * ZP];   // stage-1 output
   uint8_t sgn[NCH + 16];                      // per chunk: sign bits of its 8 samples
   uint8_t cnt[NCH + 16];                      // per chunk: crossings (low 4 bits), one into its first sample (bit 4)
-  int zc[NF + 1];                             // ZCR counts of the clip
-  uint8_t rb[NF + 1];                         // image R byte per column
-  float red[2][NWV];
+  int zc[2][NF + 1];                          // ZCR counts of the clip (double-buffered by clip)
+  float red[2][NWV];                          // per-wave max / min of the finished clip's mel power
 };
-constexpr int LB = 64 * NF;                   // image epilogue tile: 64 bands x 151 frames (float)
-static_assert(LB * sizeof(float) <= 2 * sizeof(_Float16) * 13 * TF * ZP, "epilogue tile fits Z");
 static_assert((TF - 1) * 10 + 24 < TQS && (TF - 1) * 10 + 16 + 8 + 8 <= TQ, "stage-1 reads: live / zero columns");
 static_assert(20 * (TF - 1) + 50 <= NCH, "ZCR chunks of the tile's last frame are staged");
+
+// (hi, lo) of one value in one dword: hi = f16(x) in bits 0-15, lo = f16(x - hi) in bits 16-31.
+// The hi conversions are plain C (so the compiler's hazard tracking sees the first read of an MFMA
+// result and pads it); the lo halves are v_fma_mix in inline asm, after their hi (which read the same
+// registers), rounding the exact f32 difference once -- clang turns fma(x, 1, -hi) into cvt + sub + cvt
+typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+typedef float f2v __attribute__((ext_vector_type(2)));
+MMLA_DEV uint32_t split1(float x) {   // x: a plain VALU result (staging), no MFMA hazard
+  uint32_t u;
+  asm("v_cvt_f16_f32 %0, %1\n\t"
+      "v_fma_mixhi_f16 %0, %1, 1.0, -%0 op_sel_hi:[0,0,1]"
+      : "=&v"(u) : "v"(x));
+  return u;
+}
+// two values: hi = (f16(a), f16(b)), lo = (f16(a - hi.a), f16(b - hi.b))
+MMLA_DEV void split2(float a, float b, uint32_t& hi, uint32_t& lo) {
+  hi = __builtin_bit_cast(uint32_t, __builtin_convertvector((f2v){a, b}, h2));
+  asm("v_fma_mixlo_f16 %0, %1, 1.0, -%2 op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixhi_f16 %0, %3, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+      : "=&v"(lo) : "v"(a), "v"(hi), "v"(b));
+}
 
 MMLA_DEV uint32_t pack_f16(_Float16 a, _Float16 b) {
   return (uint32_t)__builtin_bit_cast(uint16_t, a) | ((uint32_t)__builtin_bit_cast(uint16_t, b) << 16);
@@ -754,10 +777,29 @@ MMLA_DEV float wave_red(float v) {
     tlast = tn;                                                      \
   } while (0)
 #define FE3_T_STORE(clip_)                                           \
-  if (lane == 0 && (clip_) < 4096 / NWV)                             \
-    for (int i_ = 0; i_ < 8; ++i_) g_fe_t[((clip_) * NWV + wid) * 8 + i_] = tacc[i_];
+  do {                                                               \
+    if (lane == 0 && (clip_) < 4096 / NWV)                           \
+      for (int i_ = 0; i_ < 8; ++i_) g_fe_t[((clip_) * NWV + wid) * 8 + i_] = tacc[i_]; \
+    for (int i_ = 0; i_ < 8; ++i_) tacc[i_] = 0;                     \
+  } while (0)
 #endif
 
+template <int T>
+using tile_c = std::integral_constant<int, T>;
+template <class F, int... I>
+MMLA_DEV void for_tiles(F&& f, std::integer_sequence<int, I...>) {
+  (f(tile_c<I>{}), ...);
+}
+
+// Software pipeline over the workgroup's (clip, tile) steps, two barriers per step:
+//   interval A:  crossings(t), stage 1(t)  [T -> Z]      |  mel(previous step)  [P -> dB registers]
+//   interval B:  stage 2(t)  [Z -> P], ZCR sum(t)        |  staging(next step)  [PCM -> T]
+//                + at a clip's end (step (next clip, 0)): its max / min and the norm / dB / image
+//                stores straight from the registers
+// Every LDS buffer has one writer interval and one reader interval, separated by a barrier (T: B
+// writes, A reads; Z: A / B; P: B / A; sgn: B / A; cnt: A / B; zc: double-buffered by clip).  The
+// five tiles of a clip are unrolled (tile-dependent edges, offsets and dB register slots become
+// compile-time); the loop runs over the workgroup's clips plus one drain pass.
 template <bool DB, bool NM, bool IMG>
 __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_clips) {
   __shared__ __attribute__((aligned(16))) Smem sm;
@@ -784,168 +826,160 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
       a2l[j][s] = *reinterpret_cast<const f16x8*>(tb.a2[k2][s][1][lane]);
     }
   }
-  for (int i = tid; i < 128 * MW; i += NTH) sm.mw[i] = i % MW < 10 ? tb.mel_w[i / MW][i % MW] : 0.0f;
-  for (int i = tid; i < 128; i += NTH) sm.mst[i] = tb.mel_start[i];
+  for (int i = tid; i < 128 * MW; i += NTH) sm.mw[i] = i % MW < 10 ? tb.mel_w[i / MW][i % MW] * P_SCALE : 0.0f;
+  for (int i = tid; i < 128; i += NTH) sm.mst[i] = tb.mel_start[i] * PP;
   for (int i = tid; i < (PROWS - 201) * PP; i += NTH) sm.p[201 * PP + i] = 0.0f;
   for (int i = tid; i < 16 * (TP - TQS); i += NTH) sm.t[(i / (TP - TQS)) * TP + TQS + i % (TP - TQS)] = 0u;
 
-  // the next tile's 8 samples of this thread's chunk, one tile ahead: the 16-B load of the chunk
+  // an opaque copy of the thread id per use: the tile-unrolled code otherwise hoists every
+  // thread-derived address of all tiles out of the clip loop (hundreds of live registers -> spills)
+  auto otid = [&]() {
+    int v = tid;
+    asm volatile("" : "+v"(v));
+    return v;
+  };
+
+  // clip facts the staging needs, wave-uniform
+  struct ClipIn {
+    const int16_t* src;
+    int len;
+    bool fast;    // int16 PCM at a 16-B aligned start: 16-B chunk loads
+  };
+  auto clip_in = [&](int64_t clip) -> ClipIn {
+    ClipIn ci;
+    int len = a.lens ? a.lens[clip] : a.clip_len;
+    ci.len = len < 0 ? 0 : (len > CLIP ? CLIP : len);
+    ci.src = a.pcm + clip * a.clip_stride;
+    ci.fast = !a.pcm_f32 && (reinterpret_cast<uintptr_t>(ci.src) & 15) == 0;
+    return ci;
+  };
+
+  // the next staging's 8 samples of this thread's chunk, one step ahead: the 16-B load of the chunk
   // when it lies inside the clip's readable samples, else zeros (reflect-padded and partial chunks
   // are completed at staging time).  Tile 4 maps chunk c to thread c + 9 so that the reflected
   // chunks at its end and the chunks they mirror are lanes of one wave (tile 0: chunk c = thread c).
   uint32_t nx[4] = {0, 0, 0, 0};
-  auto prefetch = [&](int64_t clip_, int t_) {
+  auto prefetch = [&](int64_t clip_, auto T_) {
+    constexpr int t = decltype(T_)::value;
     nx[0] = nx[1] = nx[2] = nx[3] = 0u;
-    if (clip_ >= n_clips || a.pcm_f32) return;   // float PCM: loaded at staging time
-    const int c = tid - (t_ == NTILE - 1 ? ROT4 : 0);
-    const int i0 = HOP * TF * t_ - N_FFT / 2 + 8 * c;
-    const int16_t* s_ = a.pcm + clip_ * a.clip_stride;
-    if (c < 0 || c >= NCH || i0 < 0 || (reinterpret_cast<uintptr_t>(s_) & 15) != 0) return;
-    int len_ = a.lens ? a.lens[clip_] : a.clip_len;
-    len_ = len_ < 0 ? 0 : (len_ > CLIP ? CLIP : len_);
-    if (i0 + 8 <= len_) {
-      const uint4 v = *reinterpret_cast<const uint4*>(s_ + i0);
+    if (clip_ >= n_clips) return;
+    const ClipIn ci = clip_in(clip_);
+    if (!ci.fast) return;
+    const int c = otid() - (t == NTILE - 1 ? ROT4 : 0);
+    const int i0 = HOP * TF * t - N_FFT / 2 + 8 * c;
+    if (c >= 0 && c < NCH && i0 >= 0 && i0 + 8 <= ci.len) {
+      const uint4 v = *reinterpret_cast<const uint4*>(ci.src + i0);
       nx[0] = v.x;
       nx[1] = v.y;
       nx[2] = v.z;
       nx[3] = v.w;
     }
   };
-  prefetch(blockIdx.x, 0);
-  // mel band pairs of this wave (2 ib + hh is this lane's band) and their wave-uniform tap counts
-  int pair[PPW], ptaps[PPW];
-#pragma unroll
-  for (int k = 0; k < PPW; ++k) {
-    pair[k] = __builtin_amdgcn_readfirstlane(tb.mel_pair[NWV][wid * PPW + k]);
-    ptaps[k] = __builtin_amdgcn_readfirstlane(tb.mel_pair_taps[pair[k]]);
-  }
 
-  for (int64_t clip = blockIdx.x; clip < n_clips; clip += gridDim.x) {
-    FE3_T_INIT
-    // lane-derived offsets are recomputed per clip from an opaque copy of the lane id: hoisted out of
-    // the clip loop, the per-band store / LDS addresses stayed live across it and spilled
-    int lane_o = lane;
-    asm volatile("" : "+v"(lane_o));
-    const int r = lane_o & 31, hh = lane_o >> 5;
-    int len = a.lens ? a.lens[clip] : a.clip_len;
-    len = len < 0 ? 0 : (len > CLIP ? CLIP : len);
-    const int16_t* src = a.pcm + clip * a.clip_stride;
-    const bool vec_clip = (reinterpret_cast<uintptr_t>(src) & 15) == 0;
-    // 10 log10 S of this lane's band of each pair at frame 32 t + r; tile t lands in
-    // dbv[NTILE - 1] and moves down one slot per tile (constant indices keep dbv in registers
-    // without unrolling the tile loop; after the last tile, tile t sits at dbv[t])
-    float dbv[NTILE][PPW] = {};
-    float smax = 0.0f, smin = INFINITY;
-
-#pragma unroll 1
-    for (int t = 0; t < NTILE; ++t) {
-      const int f0 = TF * t;
-      const int ibase = HOP * f0 - N_FFT / 2;   // sample index of tile position p = 0
+  // ---- staging of (clip, t): chunk c holds p = 8c .. 8c + 7 (reflect-padded, zero past len), split
+  //      x' = x 2^-12 into fp16 hi + lo, transposed store T[p & 15][p >> 4] = (hi, lo) ---------------
+  auto stage = [&](int64_t clip, auto T_) {
+    constexpr int t = decltype(T_)::value;
+    if constexpr (FE3_SKIP & 1) return;
+    const ClipIn ci = clip_in(clip);
+    const int c = otid() - (t == NTILE - 1 ? ROT4 : 0);
+    const int i0 = HOP * TF * t - N_FFT / 2 + 8 * c;
+    const bool live = c >= 0 && c < NCH;
+    uint32_t d[8];               // (hi, lo) of x' = x 2^-12 (int16 PCM) or y 2^3 (float PCM, y = x / 32768)
+    uint32_t sg = 0;             // sign bits (librosa zero_crossings: |y| <= 1e-10 counts as 0)
+    if (!ci.fast) {
+      // float PCM or a clip start off 16-B alignment: per-sample loads (not the hot path)
 #pragma unroll
-      for (int u = 0; u + 1 < NTILE; ++u)
-#pragma unroll
-        for (int k = 0; k < PPW; ++k) dbv[u][k] = dbv[u + 1][k];
-      // ---- stage the tile: chunk c holds p = 8c .. 8c + 7 (reflect-padded, zero past len), split
-      //      x' = x 2^-12 into fp16 hi + lo, transposed store T[p & 15][p >> 4] = (hi, lo) ------
-      if constexpr (!(FE3_SKIP & 1)) {
-        const int c = tid - (t == NTILE - 1 ? ROT4 : 0);
-        const int i0 = ibase + 8 * c;
-        const bool live = c >= 0 && c < NCH;
-        float xs[8];                 // x' = x 2^-12 (int16 PCM) or y 2^3 (float PCM, y = x / 32768)
-        uint32_t sg = 0;             // sign bits (librosa zero_crossings: |y| <= 1e-10 counts as 0)
-        if (a.pcm_f32 || !vec_clip) {
-          // float PCM or a clip start off 16-B alignment: per-sample loads (not the hot path)
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            int i = i0 + j;
-            i = i < 0 ? -i : i;
-            i = i >= CLIP ? 2 * (CLIP - 1) - i : i;
-            const bool in = live && i >= 0 && i < len;
-            if (a.pcm_f32) {
-              const float y = in ? a.pcm_f32[clip * a.clip_stride + i] : 0.0f;
-              xs[j] = y * (32768.0f * X_SCALE);
-              sg |= (uint32_t)(y < -1e-10f) << j;
-            } else {
-              const int16_t v = in ? src[i] : (int16_t)0;
-              xs[j] = (float)v * X_SCALE;
-              sg |= (uint32_t)(v < 0) << j;
-            }
-          }
+      for (int j = 0; j < 8; ++j) {
+        int i = i0 + j;
+        i = i < 0 ? -i : i;
+        i = i >= CLIP ? 2 * (CLIP - 1) - i : i;
+        const bool in = live && i >= 0 && i < ci.len;
+        if (a.pcm_f32) {
+          const float y = in ? a.pcm_f32[clip * a.clip_stride + i] : 0.0f;
+          d[j] = split1(y * (32768.0f * X_SCALE));
+          sg |= (uint32_t)(y < -1e-10f) << j;
         } else {
-          uint32_t w[4] = {nx[0], nx[1], nx[2], nx[3]};
-          if (live && i0 >= 0 && i0 < len && i0 + 8 > len) {
-            // the clip's last, partial chunk: its samples one by one (once per clip)
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-              const uint32_t lo16 = i0 + 2 * k < len ? (uint16_t)src[i0 + 2 * k] : 0u;
-              const uint32_t hi16 = i0 + 2 * k + 1 < len ? (uint16_t)src[i0 + 2 * k + 1] : 0u;
-              w[k] = lo16 | (hi16 << 16);
-            }
-          }
-          // reflect padding (center=True, pad_mode='reflect') of the zero-padded 24000 samples: the
-          // chunks before sample 0 (tile 0, chunks 0..24) and past sample 23999 (tile 4, chunks
-          // 465..489) take their samples from the chunks they mirror, lanes of the same wave:
-          //   tile 0: p' = 400 - p  -> chunk 49 - c elements 8 - j (j >= 1), chunk 50 - c element 0
-          //   tile 4: p' = 7438 - p -> chunk 929 - c elements 6 - j (j <= 6), chunk 928 - c element 7
-          if ((t == 0 && wid == 0) || (t == NTILE - 1 && wid == (465 + ROT4) / 64)) {
-            const bool first = t == 0;
-            const int pa = first ? 49 - c : 929 - c, pb = first ? 50 - c : 928 - c;
-            const int la = (pa + (first ? 0 : ROT4)) & 63, lb = (pb + (first ? 0 : ROT4)) & 63;
-            uint32_t ma[4], mb;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) ma[k] = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * la, (int)w[k]);
-            mb = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * lb, (int)w[first ? 0 : 3]);
-            const bool refl = first ? (c < 25) : (c >= 465 && c < 490);
-            if (refl) {
-              auto el = [&](int e) -> uint32_t { return (ma[e >> 1] >> (16 * (e & 1))) & 0xffffu; };
-              uint32_t v[8];
-              if (first) {
-                v[0] = mb & 0xffffu;
-#pragma unroll
-                for (int jj = 1; jj < 8; ++jj) v[jj] = el(8 - jj);
-              } else {
-#pragma unroll
-                for (int jj = 0; jj < 7; ++jj) v[jj] = el(6 - jj);
-                v[7] = mb >> 16;
-              }
-#pragma unroll
-              for (int k = 0; k < 4; ++k) w[k] = v[2 * k] | (v[2 * k + 1] << 16);
-            }
-          }
-          if (!live || i0 >= CLIP + N_FFT / 2) w[0] = w[1] = w[2] = w[3] = 0u;   // past the padded signal
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            xs[2 * k] = (float)(int16_t)(w[k] & 0xffffu) * X_SCALE;
-            xs[2 * k + 1] = (float)(int16_t)(w[k] >> 16) * X_SCALE;
-          }
-          // sign bits: the high byte of each sample gathered (perm), bit 7 of each byte packed
-          const uint32_t h01 = __builtin_amdgcn_perm(w[1], w[0], 0x07050301u);
-          const uint32_t h23 = __builtin_amdgcn_perm(w[3], w[2], 0x07050301u);
-          sg = ((((h01 >> 7) & 0x01010101u) * 0x01020408u) >> 24) |
-               (((((h23 >> 7) & 0x01010101u) * 0x01020408u) >> 24) << 4);
-        }
-        if (live) {
-          const int n1b = (c & 1) * 8, q = c >> 1;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const _Float16 hi = (_Float16)xs[j];
-            sm.t[(n1b + j) * TP + q] = pack_f16(hi, (_Float16)(xs[j] - (float)hi));
-          }
-          sm.sgn[c] = (uint8_t)sg;
+          const int16_t v = in ? ci.src[i] : (int16_t)0;
+          d[j] = split1((float)v * X_SCALE);
+          sg |= (uint32_t)(v < 0) << j;
         }
       }
-      if (t + 1 < NTILE) prefetch(clip, t + 1);
-      else prefetch(clip + gridDim.x, 0);
-      FE3_MARK(0);
-      __syncthreads();
-      FE3_MARK(1);
+    } else {
+      uint32_t w[4] = {nx[0], nx[1], nx[2], nx[3]};
+      if (ci.len < CLIP && live && i0 >= 0 && i0 < ci.len && i0 + 8 > ci.len) {
+        // the clip's last, partial chunk: its samples one by one (short clips only)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const uint32_t lo16 = i0 + 2 * k < ci.len ? (uint16_t)ci.src[i0 + 2 * k] : 0u;
+          const uint32_t hi16 = i0 + 2 * k + 1 < ci.len ? (uint16_t)ci.src[i0 + 2 * k + 1] : 0u;
+          w[k] = lo16 | (hi16 << 16);
+        }
+      }
+      // reflect padding (center=True, pad_mode='reflect') of the zero-padded 24000 samples: the
+      // chunks before sample 0 (tile 0, chunks 0..24) and past sample 23999 (tile 4, chunks
+      // 465..489) take their samples from the chunks they mirror, lanes of the same wave:
+      //   tile 0: p' = 400 - p  -> chunk 49 - c elements 8 - j (j >= 1), chunk 50 - c element 0
+      //   tile 4: p' = 7438 - p -> chunk 929 - c elements 6 - j (j <= 6), chunk 928 - c element 7
+      if constexpr (t == 0 || t == NTILE - 1) {
+        constexpr bool first = t == 0;
+        if (wid == (first ? 0 : (465 + ROT4) / 64)) {
+          const int pa = first ? 49 - c : 929 - c, pb = first ? 50 - c : 928 - c;
+          const int la = (pa + (first ? 0 : ROT4)) & 63, lb = (pb + (first ? 0 : ROT4)) & 63;
+          uint32_t ma[4], mb;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) ma[k] = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * la, (int)w[k]);
+          mb = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * lb, (int)w[first ? 0 : 3]);
+          const bool refl = first ? (c < 25) : (c >= 465 && c < 490);
+          if (refl) {
+            auto el = [&](int e) -> uint32_t { return (ma[e >> 1] >> (16 * (e & 1))) & 0xffffu; };
+            uint32_t v[8];
+            if (first) {
+              v[0] = mb & 0xffffu;
+#pragma unroll
+              for (int jj = 1; jj < 8; ++jj) v[jj] = el(8 - jj);
+            } else {
+#pragma unroll
+              for (int jj = 0; jj < 7; ++jj) v[jj] = el(6 - jj);
+              v[7] = mb >> 16;
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) w[k] = v[2 * k] | (v[2 * k + 1] << 16);
+          }
+        }
+      }
+      if constexpr (t == NTILE - 1) {
+        if (!live || i0 >= CLIP + N_FFT / 2) w[0] = w[1] = w[2] = w[3] = 0u;   // past the padded signal
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        d[2 * k] = split1((float)(int16_t)(w[k] & 0xffffu) * X_SCALE);
+        d[2 * k + 1] = split1((float)(int16_t)(w[k] >> 16) * X_SCALE);
+      }
+      // sign bits: the high byte of each sample gathered (perm), bit 7 of each byte packed
+      const uint32_t h01 = __builtin_amdgcn_perm(w[1], w[0], 0x07050301u);
+      const uint32_t h23 = __builtin_amdgcn_perm(w[3], w[2], 0x07050301u);
+      sg = ((((h01 >> 7) & 0x01010101u) * 0x01020408u) >> 24) |
+           (((((h23 >> 7) & 0x01010101u) * 0x01020408u) >> 24) << 4);
+    }
+    if (live) {
+      uint32_t* tq = sm.t + (c & 1) * 8 * TP + (c >> 1);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) tq[j * TP] = d[j];
+      sm.sgn[c] = (uint8_t)sg;
+    }
+  };
 
-      // ---- crossings per chunk: transitions into its 8 samples, counted for samples 1 <= i <=
-      //      CLIP - 1 (edge padding repeats the clip's first / last sample: no crossing there) -------
-      for (int c = tid; c < NCH; c += NTH) {
-        const uint32_t m = sm.sgn[c];
-        const uint32_t pv = c > 0 ? (uint32_t)sm.sgn[c - 1] >> 7 : 0u;
-        uint32_t tr = (m ^ ((m << 1) | pv)) & 0xffu;
+  // ---- crossings per chunk of tile t: transitions into its 8 samples, counted for samples
+  //      1 <= i <= CLIP - 1 (edge padding repeats the clip's first / last sample: no crossing) ------
+  auto crossings = [&](auto T_) {
+    constexpr int t = decltype(T_)::value;
+    const int ibase = HOP * TF * t - N_FFT / 2;
+    for (int c = otid(); c < NCH; c += NTH) {
+      const uint32_t m = sm.sgn[c];
+      const uint32_t pv = c > 0 ? (uint32_t)sm.sgn[c - 1] >> 7 : 0u;
+      uint32_t tr = (m ^ ((m << 1) | pv)) & 0xffu;
+      if constexpr (t == 0 || t == NTILE - 1) {
         const int i0 = ibase + 8 * c;
         if (i0 < 1 || i0 + 7 > CLIP - 1) {
           uint32_t vm = 0;
@@ -953,253 +987,283 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
           for (int j = 0; j < 8; ++j) vm |= (uint32_t)(i0 + j >= 1 && i0 + j <= CLIP - 1) << j;
           tr &= vm;
         }
-        sm.cnt[c] = (uint8_t)(__builtin_popcount(tr) | ((tr & 1u) << 4));
       }
+      sm.cnt[c] = (uint8_t)(__builtin_popcount(tr) | ((tr & 1u) << 4));
+    }
+  };
 
-      // ---- stage 1 (wave = n1 G1 wid .. + G1 - 1): D1 = A1[n1] (32 x 32) . B1 (32 n2 x 32 frames) ----
-      if constexpr (!(FE3_SKIP & 2)) {
-        f32x16 acc[G1];
+  // ---- stage 1 (wave = n1 G1 wid .. + G1 - 1): D1 = A1[n1] (32 x 32) . B1 (32 n2 x 32 frames) ------
+  auto stage1 = [&](int r, int hh) {
+    if constexpr (FE3_SKIP & 2) return;
+    f32x16 acc[G1];
 #pragma unroll
-        for (int g = 0; g < G1; ++g) {
-          const int n1 = G1 * wid + g;
-          // lane (frame r, half hh): q = 10 r + 16 s + 8 hh + j, j < 8 (two 8-B reads per 4 pairs)
-          const uint2* tp = reinterpret_cast<const uint2*>(sm.t + n1 * TP + 10 * r + 8 * hh);
-          acc[g] = f32x16{};
+    for (int g = 0; g < G1; ++g) {
+      const int n1 = G1 * wid + g;
+      // lane (frame r, half hh): q = 10 r + 16 s + 8 hh + j, j < 8 (two 8-B reads per 4 pairs)
+      const uint2* tp = reinterpret_cast<const uint2*>(sm.t + n1 * TP + 10 * r + 8 * hh);
+      acc[g] = f32x16{};
 #pragma unroll
-          for (int s = 0; s < 2; ++s) {
-            uint32_t w[8];
+      for (int s = 0; s < 2; ++s) {
+        uint32_t w[8];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              const uint2 d = tp[8 * s + i];
-              w[2 * i] = d.x;
-              w[2 * i + 1] = d.y;
-            }
-            uint32_t bh[4], bl[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {   // de-interleave (hi, lo) pairs: bytes 0-1 / 2-3 of each word
-              bh[i] = __builtin_amdgcn_perm(w[2 * i + 1], w[2 * i], 0x05040100u);
-              bl[i] = __builtin_amdgcn_perm(w[2 * i + 1], w[2 * i], 0x07060302u);
-            }
-            const f16x8 BH = __builtin_bit_cast(f16x8, bh), BL = __builtin_bit_cast(f16x8, bl);
-            acc[g] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1l[g][s], BH, acc[g], 0, 0, 0);
-            acc[g] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1h[g][s], BL, acc[g], 0, 0, 0);
-            acc[g] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1h[g][s], BH, acc[g], 0, 0, 0);
-          }
+        for (int i = 0; i < 4; ++i) {
+          const uint2 dd = tp[8 * s + i];
+          w[2 * i] = dd.x;
+          w[2 * i + 1] = dd.y;
         }
-        // registers 2 pi, 2 pi + 1 = (re, im) of Y_n1[k2], k2 = (pi & 1) + 4 (pi >> 1) + 2 hh, for
-        // frame r: split hi / lo into Z[k2][r][2 n1 ..] (the wave's G1 n1 are 2 G1 consecutive k)
-        uint32_t* zh = reinterpret_cast<uint32_t*>(sm.z_hi) + r * (ZP / 2) + G1 * wid;
-        uint32_t* zl = reinterpret_cast<uint32_t*>(sm.z_lo) + r * (ZP / 2) + G1 * wid;
-        // k2 < 13 except (pi 7: both halves) and (pi 6, hh 1: k2 14) -- that one goes to a trash word
+        uint32_t bh[4], bl[4];
 #pragma unroll
-        for (int pi = 0; pi < 7; ++pi) {
-          const int k2 = (pi & 1) + 4 * (pi >> 1) + 2 * hh;
-          if (pi == 6) {
-            const float re = acc[0][12], im = acc[0][13];
-            const _Float16 hre = (_Float16)(re * Y_SCALE), him = (_Float16)(im * Y_SCALE);
-            const uint32_t vh = pack_f16(hre, him);
-            const uint32_t vl = pack_f16((_Float16)__builtin_fmaf(re, Y_SCALE, -(float)hre),
-                                         (_Float16)__builtin_fmaf(im, Y_SCALE, -(float)him));
-            uint32_t* th = hh ? &sm.ztrash[lane] : zh + 12 * TF * (ZP / 2);
-            uint32_t* tl = hh ? &sm.ztrash[64 + lane] : zl + 12 * TF * (ZP / 2);
-            *th = vh;
-            *tl = vl;
-            continue;
-          }
-          {
-            uint32_t vh[G1], vl[G1];
+        for (int i = 0; i < 4; ++i) {   // de-interleave (hi, lo) pairs: bytes 0-1 / 2-3 of each word
+          bh[i] = __builtin_amdgcn_perm(w[2 * i + 1], w[2 * i], 0x05040100u);
+          bl[i] = __builtin_amdgcn_perm(w[2 * i + 1], w[2 * i], 0x07060302u);
+        }
+        const f16x8 BH = __builtin_bit_cast(f16x8, bh), BL = __builtin_bit_cast(f16x8, bl);
+        acc[g] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1l[g][s], BH, acc[g], 0, 0, 0);
+        acc[g] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1h[g][s], BL, acc[g], 0, 0, 0);
+        acc[g] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1h[g][s], BH, acc[g], 0, 0, 0);
+      }
+    }
+    // registers 2 pi, 2 pi + 1 = (re, im) of Y_n1[k2], k2 = (pi & 1) + 4 (pi >> 1) + 2 hh, for
+    // frame r: split hi / lo into Z[k2][r][2 n1 ..] (the wave's G1 n1 are 2 G1 consecutive k)
+    uint32_t* zh = reinterpret_cast<uint32_t*>(sm.z_hi) + r * (ZP / 2) + G1 * wid;
+    uint32_t* zl = reinterpret_cast<uint32_t*>(sm.z_lo) + r * (ZP / 2) + G1 * wid;
+    // k2 < 13 except (pi 7: both halves) and (pi 6, hh 1: k2 14) -- that one goes to a trash word
 #pragma unroll
-            for (int g = 0; g < G1; ++g) {
-              // hi = f16(2 y), lo = f16(2 y - hi): each one fused multiply-add into a half (fma_mix)
-              const float re = acc[g][2 * pi], im = acc[g][2 * pi + 1];
-              const _Float16 hre = (_Float16)(re * Y_SCALE), him = (_Float16)(im * Y_SCALE);
-              vh[g] = pack_f16(hre, him);
-              vl[g] = pack_f16((_Float16)__builtin_fmaf(re, Y_SCALE, -(float)hre),
-                               (_Float16)__builtin_fmaf(im, Y_SCALE, -(float)him));
-            }
-            if constexpr (G1 == 2) {
-              *reinterpret_cast<uint2*>(zh + k2 * TF * (ZP / 2)) = uint2{vh[0], vh[1]};
-              *reinterpret_cast<uint2*>(zl + k2 * TF * (ZP / 2)) = uint2{vl[0], vl[1]};
-            } else {
-              zh[k2 * TF * (ZP / 2)] = vh[0];
-              zl[k2 * TF * (ZP / 2)] = vl[0];
-            }
-          }
+    for (int pi = 0; pi < 7; ++pi) {
+      const int k2 = (pi & 1) + 4 * (pi >> 1) + 2 * hh;
+      uint32_t vh[G1], vl[G1];
+#pragma unroll
+      for (int g = 0; g < G1; ++g) split2(acc[g][2 * pi], acc[g][2 * pi + 1], vh[g], vl[g]);
+      if (pi == 6) {
+        uint32_t* th = hh ? &sm.ztrash[lane] : zh + 12 * TF * (ZP / 2);
+        uint32_t* tl = hh ? &sm.ztrash[64 + lane] : zl + 12 * TF * (ZP / 2);
+        *th = vh[0];
+        *tl = vl[0];
+      } else if constexpr (G1 == 2) {
+        *reinterpret_cast<uint2*>(zh + k2 * TF * (ZP / 2)) = uint2{vh[0], vh[1]};
+        *reinterpret_cast<uint2*>(zl + k2 * TF * (ZP / 2)) = uint2{vl[0], vl[1]};
+      } else {
+        zh[k2 * TF * (ZP / 2)] = vh[0];
+        zl[k2 * TF * (ZP / 2)] = vl[0];
+      }
+    }
+  };
+
+  // ---- stage 2 (wave = k2' wid + NWV j): D2 = A2[k2'] (32 x 32) . Z[k2'] (32 k x 32 frames)
+  //      -> |X|^2 (x 2^38: P_SCALE sits in the mel weights) -> P[bin][frame] ------------------------
+  auto stage2 = [&](int r, int hh) {
+#pragma unroll
+    for (int j = 0; j < G2; ++j) {
+      const int k2 = wid + NWV * j;
+      if (k2 >= 13 || (FE3_SKIP & 4)) continue;
+      const _Float16* zh = sm.z_hi + (k2 * TF + r) * ZP + 8 * hh;
+      const _Float16* zl = sm.z_lo + (k2 * TF + r) * ZP + 8 * hh;
+      f32x16 acc = {};
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const f16x8 BH = *reinterpret_cast<const f16x8*>(zh + 16 * s);
+        const f16x8 BL = *reinterpret_cast<const f16x8*>(zl + 16 * s);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a2l[j][s], BH, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a2h[j][s], BL, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a2h[j][s], BH, acc, 0, 0, 0);
+      }
+      // pair i = c0 + 2 hh (c0 = (pi & 1) + 4 (pi >> 1)): bin 25 i + k2 (i < 8: c0 < 8), else
+      // 25 (i - 8) + 25 - k2; GEMM 0 has bins 25 i for i <= 8 only (the other lanes write the
+      // trash row).  Branch-free: the row offset is an immediate plus the wave-uniform k2
+      float* prow = sm.p + 50 * PP * hh + r;
+      float* trash = sm.p + PTRASH * PP + lane;
+#pragma unroll
+      for (int pi = 0; pi < 8; ++pi) {
+        const int c0 = (pi & 1) + 4 * (pi >> 1);
+        const float re = acc[2 * pi], im = acc[2 * pi + 1];
+        const float pw = fmaf(re, re, im * im);
+        if (k2 == 0) {
+          if (c0 <= 8) *(c0 + 2 * hh <= 8 ? prow + 25 * c0 * PP : trash) = pw;
+        } else if (c0 < 8) {
+          prow[(25 * c0 + k2) * PP] = pw;
+        } else {
+          prow[(25 * (c0 - 8) + 25 - k2) * PP] = pw;
+        }
+      }
+    }
+  };
+
+  // ---- ZCR of tile t (last wave): frame f0 + lane = the transitions into tile positions
+  //      160 lane + 1 .. + 399 = chunks 20 lane .. 20 lane + 49 minus the one into chunk 20 lane's
+  //      first sample ---------------------------------------------------------------------------------
+  auto zsum = [&](auto T_, int par) {
+    constexpr int t = decltype(T_)::value;
+    if (wid == NWV - 1 && lane < TF) {
+      const uint32_t* cw = reinterpret_cast<const uint32_t*>(sm.cnt) + 5 * lane;
+      int s = 0;
+#pragma unroll
+      for (int k = 0; k < 13; ++k) {
+        const uint32_t w = cw[k] & (k == 12 ? 0x0f0fu : 0x0f0f0f0fu);
+        s += (int)((w * 0x01010101u) >> 24);
+      }
+      s -= (int)((cw[0] >> 4) & 1u);
+      if (TF * t + lane < NF) sm.zc[par][TF * t + lane] = s;
+    }
+  };
+
+  // mel band pairs of this wave (2 ib + hh is this lane's band) and their wave-uniform tap counts
+  int pair[PPW], ptaps[PPW];
+#pragma unroll
+  for (int k = 0; k < PPW; ++k) {
+    pair[k] = __builtin_amdgcn_readfirstlane(tb.mel_pair[NWV][wid * PPW + k]);
+    ptaps[k] = __builtin_amdgcn_readfirstlane(tb.mel_pair_taps[pair[k]]);
+  }
+  // 10 log10 S of this lane's band of each pair at frame 32 t + r
+  float dbv[NTILE][PPW];
+  float smax = 0.0f, smin = INFINITY;
+
+  // ---- mel of tile t (lane = frame r x band 2 ib + hh of each of the wave's pairs ib; the pair's tap
+  //      count is wave-uniform, taps past a band's own count are zero weights) -> 10 log10 S --------
+  auto mel = [&](auto T_, int r, int hh) {
+    constexpr int t = decltype(T_)::value;
+#pragma unroll
+    for (int k = 0; k < PPW; ++k) {
+      if (FE3_SKIP & 8) break;
+      const int b = 2 * pair[k] + hh;
+      const float* wp = sm.mw + b * MW;
+      const float* pp = sm.p + sm.mst[b] + r;
+      float sacc = 0.0f;
+      // taps in batches of 4 (the batch's reads issued before its FMAs): zero weights past the
+      // band's own taps, P rows past bin 200 are zero
+#pragma unroll
+      for (int j0 = 0; j0 < MW; j0 += 4) {
+        if (j0 >= ptaps[k]) break;
+        const float4 w4 = *reinterpret_cast<const float4*>(wp + j0);
+        const float p0 = pp[j0 * PP], p1 = pp[(j0 + 1) * PP], p2 = pp[(j0 + 2) * PP], p3 = pp[(j0 + 3) * PP];
+        sacc = fmaf(w4.x, p0, sacc);
+        sacc = fmaf(w4.y, p1, sacc);
+        sacc = fmaf(w4.z, p2, sacc);
+        sacc = fmaf(w4.w, p3, sacc);
+      }
+      dbv[t][k] = db10(sacc);
+      if (TF * t + TF <= NF || TF * t + r < NF) {
+        smax = fmaxf(smax, sacc);
+        smin = fminf(smin, sacc);
+      }
+    }
+  };
+
+  // ---- a clip's end: max / min of its mel power over the waves, power_to_db(ref=np.max, amin=1e-10,
+  //      top_db=80) with numpy-1.21 dtypes, normalize_matrix (max / min of the dB matrix are the dB
+  //      of max / min S, as v2), stores straight from the registers -----------------------------------
+  auto epilogue = [&](int64_t clip, int par, int r, int hh) {
+#pragma clang fp contract(off)
+    float mx = sm.red[0][0], mn = sm.red[1][0];
+#pragma unroll
+    for (int w = 1; w < NWV; ++w) {
+      mx = fmaxf(mx, sm.red[0][w]);
+      mn = fminf(mn, sm.red[1][w]);
+    }
+    const float ref_db = (float)(10.0 * log10(fmax(1e-10, (double)mx)));
+    const float d_max = db10(mx) - ref_db;
+    const float thr = d_max - 80.0f;
+    const float d_min = fmaxf(db10(mn) - ref_db, thr);
+    const float diff = d_max - d_min;
+    const float inv_diff = 1.0f / diff;
+    const int tz = otid();
+    if (a.zcr && tz < NF) a.zcr[clip * NF + tz] = (float)sm.zc[par][tz] * (1.0f / 400.0f);
+    // norm / dB rows: lane (r, hh) of a pair writes frame 32 t + r of band 2 ib + hh -- 128 B of
+    // one band row per half-wave.  Image (rows h = 127 - band, RGB bytes): R = trunc(255 zcr[w]),
+    // G = B = trunc(255 (1 - norm)) in float64, NaN -> 0; three byte stores per pixel
+    const int64_t ob = clip * (int64_t)(NMEL * NF) + r;
+#pragma unroll
+    for (int k = 0; k < PPW; ++k) {
+      const int b = 2 * pair[k] + hh;
+      float* qn = NM ? a.norm + ob + b * NF : nullptr;
+      float* qd = DB ? a.db + ob + b * NF : nullptr;
+      uint8_t* qi = IMG ? a.img + clip * (int64_t)(NMEL * NF * 3) + ((NMEL - 1 - b) * NF + r) * 3 : nullptr;
+#pragma unroll
+      for (int t = 0; t < NTILE; ++t) {
+        if (TF * t + TF > NF && TF * t + r >= NF) continue;
+        const float d = fmaxf(dbv[t][k] - ref_db, thr);
+        // (d - min) / (max - min) as a multiply by the reciprocal (<= 2 ulp; as v2); 0 * inf =
+        // NaN keeps the digital-silence NaN
+        const float nv = (d - d_min) * inv_diff;
+        if (NM && !(FE3_SKIP & 16)) qn[TF * t] = nv;
+        if (DB) qd[TF * t] = d;
+        if (IMG) {
+          const double v = (1.0 - (double)nv) * 255.0;
+          const uint8_t gb = (v >= 0.0) ? (uint8_t)((uint32_t)(int)v & 255u) : (uint8_t)0;
+          const uint8_t rr = (uint8_t)(int)(((double)sm.zc[par][TF * t + r] / 400.0) * 255.0);
+          qi[3 * TF * t] = rr;
+          qi[3 * TF * t + 1] = gb;
+          qi[3 * TF * t + 2] = gb;
+        }
+      }
+    }
+  };
+
+  const int64_t my_clips = (int64_t)blockIdx.x < n_clips ? (n_clips - 1 - blockIdx.x) / gridDim.x + 1 : 0;
+  FE3_T_INIT
+  if (my_clips > 0) {
+    prefetch(blockIdx.x, tile_c<0>{});
+    stage(blockIdx.x, tile_c<0>{});
+    prefetch(blockIdx.x, tile_c<1>{});
+  }
+  __syncthreads();
+
+#pragma unroll 1
+  for (int64_t ci = 0; ci <= my_clips; ++ci) {
+    const int64_t clip = blockIdx.x + ci * gridDim.x;
+    const bool cur = ci < my_clips;
+    const int par = (int)(ci & 1);
+    for_tiles([&](auto T_) {
+      constexpr int t = decltype(T_)::value;
+      if (!cur && t > 0) return;
+      // lane-derived offsets are recomputed per tile from an opaque copy of the lane id: hoisted,
+      // the per-band store / LDS addresses of all five tiles stay live together and spill
+      int lane_o = lane;
+      asm volatile("" : "+v"(lane_o));
+      const int r = lane_o & 31, hh = lane_o >> 5;
+      // ---- interval A ----
+      if (cur) {
+        crossings(T_);
+        stage1(r, hh);
+      }
+      if constexpr (t > 0) {
+        mel(tile_c<t - 1>{}, r, hh);
+      } else if (ci > 0) {
+        mel(tile_c<NTILE - 1>{}, r, hh);
+        const float mx = wave_red<true>(smax), mn = wave_red<false>(smin);
+        if (lane == 0) {
+          sm.red[0][wid] = mx;
+          sm.red[1][wid] = mn;
+        }
+        smax = 0.0f;
+        smin = INFINITY;
+      }
+      FE3_MARK(0);
+      __syncthreads();
+      FE3_MARK(1);
+      // ---- interval B ----
+      if (cur) {
+        stage2(r, hh);
+        zsum(T_, par);
+        if constexpr (t + 1 < NTILE) {
+          stage(clip, tile_c<t + 1>{});
+        } else if (ci + 1 < my_clips) {
+          stage(clip + gridDim.x, tile_c<0>{});
+        }
+        if constexpr (t + 2 < NTILE) {
+          prefetch(clip, tile_c<t + 2>{});
+        } else {
+          prefetch(ci + 1 < my_clips ? clip + gridDim.x : n_clips, tile_c<t + 2 - NTILE>{});
         }
       }
       FE3_MARK(2);
-      __syncthreads();
+      if (t == 0 && ci > 0) {
+        epilogue(clip - gridDim.x, par ^ 1, r, hh);
+        FE3_MARK(4);
+        FE3_T_STORE(clip - gridDim.x);
+      }
+      if (cur) __syncthreads();
       FE3_MARK(3);
-
-      // ---- stage 2 (wave = k2' wid + NWV j): D2 = A2[k2'] (32 x 32) . Z[k2'] (32 k x 32 frames)
-      //      -> |X|^2 -> P[bin][frame]; the last wave also sums the tile's crossings per frame ------
-#pragma unroll
-      for (int j = 0; j < G2; ++j) {
-        const int k2 = wid + NWV * j;
-        if (k2 >= 13 || (FE3_SKIP & 4)) continue;
-        const _Float16* zh = sm.z_hi + (k2 * TF + r) * ZP + 8 * hh;
-        const _Float16* zl = sm.z_lo + (k2 * TF + r) * ZP + 8 * hh;
-        f32x16 acc = {};
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          const f16x8 BH = *reinterpret_cast<const f16x8*>(zh + 16 * s);
-          const f16x8 BL = *reinterpret_cast<const f16x8*>(zl + 16 * s);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a2l[j][s], BH, acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a2h[j][s], BL, acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a2h[j][s], BH, acc, 0, 0, 0);
-        }
-        // pair i = c0 + 2 hh (c0 = (pi & 1) + 4 (pi >> 1)): bin 25 i + k2 (i < 8: c0 < 8), else
-        // 25 (i - 8) + 25 - k2; GEMM 0 has bins 25 i for i <= 8 only (the other lanes write the
-        // trash row).  Branch-free: the row offset is an immediate plus the wave-uniform k2
-        float* prow = sm.p + 50 * PP * hh + r;
-        float* trash = sm.p + PTRASH * PP + lane;
-#pragma unroll
-        for (int pi = 0; pi < 8; ++pi) {
-          const int c0 = (pi & 1) + 4 * (pi >> 1);
-          const float re = acc[2 * pi], im = acc[2 * pi + 1];
-          const float pw = fmaf(re, re, im * im) * P_SCALE;
-          if (k2 == 0) {
-            if (c0 <= 8) *(c0 + 2 * hh <= 8 ? prow + 25 * c0 * PP : trash) = pw;
-          } else if (c0 < 8) {
-            prow[(25 * c0 + k2) * PP] = pw;
-          } else {
-            prow[(25 * (c0 - 8) + 25 - k2) * PP] = pw;
-          }
-        }
-      }
-      if (wid == NWV - 1 && lane < TF) {
-        // frame f0 + lane: the transitions into tile positions 160 lane + 1 .. + 399 = chunks
-        // 20 lane .. 20 lane + 49 minus the one into the chunk-20-lane's first sample
-        const uint32_t* cw = reinterpret_cast<const uint32_t*>(sm.cnt) + 5 * lane;
-        int s = 0;
-#pragma unroll
-        for (int k = 0; k < 13; ++k) {
-          const uint32_t w = cw[k] & (k == 12 ? 0x0f0fu : 0x0f0f0f0fu);
-          s += (int)((w * 0x01010101u) >> 24);
-        }
-        s -= (int)((cw[0] >> 4) & 1u);
-        if (f0 + lane < NF) sm.zc[f0 + lane] = s;
-      }
-      FE3_MARK(4);
-      __syncthreads();
-      FE3_MARK(5);
-
-      // ---- mel (lane = frame r x band 2 ib + hh of each of the wave's pairs ib; the pair's tap
-      //      count is wave-uniform, taps past a band's own count are zero weights) -> 10 log10 S ----
-#pragma unroll
-      for (int k = 0; k < PPW; ++k) {
-        if (FE3_SKIP & 8) break;
-        const int b = 2 * pair[k] + hh;
-        const float* wp = sm.mw + b * MW;
-        const float* pp = sm.p + sm.mst[b] * PP + r;
-        float sacc = 0.0f;
-        // taps in batches of 4 (all 8 reads issued before the first FMA): zero weights past the
-        // band's own taps, P rows past bin 200 are zero
-        for (int j0 = 0; j0 < ptaps[k]; j0 += 4) {
-          const float4 w4 = *reinterpret_cast<const float4*>(wp + j0);
-          const float p0 = pp[j0 * PP], p1 = pp[(j0 + 1) * PP], p2 = pp[(j0 + 2) * PP], p3 = pp[(j0 + 3) * PP];
-          sacc = fmaf(w4.x, p0, sacc);
-          sacc = fmaf(w4.y, p1, sacc);
-          sacc = fmaf(w4.z, p2, sacc);
-          sacc = fmaf(w4.w, p3, sacc);
-        }
-        dbv[NTILE - 1][k] = db10(sacc);
-        if (f0 + r < NF) {
-          smax = fmaxf(smax, sacc);
-          smin = fminf(smin, sacc);
-        }
-      }
-      FE3_MARK(6);
-    }
-
-    // ---- clip max / min of the mel power -------------------------------------------------------
-    smax = wave_red<true>(smax);
-    smin = wave_red<false>(smin);
-    if (lane == 0) {
-      sm.red[0][wid] = smax;
-      sm.red[1][wid] = smin;
-    }
-    __syncthreads();
-    smax = sm.red[0][0];
-    smin = sm.red[1][0];
-#pragma unroll
-    for (int w = 1; w < NWV; ++w) {
-      smax = fmaxf(smax, sm.red[0][w]);
-      smin = fminf(smin, sm.red[1][w]);
-    }
-    {
-#pragma clang fp contract(off)
-      // power_to_db(ref=np.max, amin=1e-10, top_db=80) with numpy-1.21 dtypes, then
-      // normalize_matrix (as v2: max / min of the dB matrix are the dB of max / min S)
-      const float ref_db = (float)(10.0 * log10(fmax(1e-10, (double)smax)));
-      const float d_max = db10(smax) - ref_db;
-      const float thr = d_max - 80.0f;
-      const float d_min = fmaxf(db10(smin) - ref_db, thr);
-      const float diff = d_max - d_min;
-      const float inv_diff = 1.0f / diff;
-
-      if (a.zcr && tid < NF) a.zcr[clip * NF + tid] = (float)sm.zc[tid] * (1.0f / 400.0f);
-      // norm / dB rows: lane (r, hh) of a pair writes frame 32 t + r of band 2 ib + hh -- 128 B of
-      // one band row per half-wave
-      const int64_t ob = clip * (int64_t)(NMEL * NF);
-#pragma unroll
-      for (int k = 0; k < PPW; ++k) {
-        const int b = 2 * pair[k] + hh;
-#pragma unroll
-        for (int t = 0; t < NTILE; ++t) {
-          const int f = TF * t + r;
-          if (f < NF) {
-            const float d = fmaxf(dbv[t][k] - ref_db, thr);
-            // (d - min) / (max - min) as a multiply by the reciprocal (<= 2 ulp; as v2); 0 * inf =
-            // NaN keeps the digital-silence NaN
-            if (NM && !(FE3_SKIP & 16)) a.norm[ob + b * NF + f] = (d - d_min) * inv_diff;
-            if (DB) a.db[ob + b * NF + f] = d;
-          }
-        }
-      }
-      if (IMG) {
-        // image: normalised values through LDS in two halves of 64 bands (rows h = 127 - m: half hb
-        // is rows h_lo .. h_lo + 63, row h_lo + hr <- band 64 hb + 63 - hr); R = trunc(255 zcr[w]),
-        // G = B = trunc(255 (1 - norm)) in float64; NaN -> 0
-        if (tid < NF) sm.rb[tid] = (uint8_t)(int)(((double)sm.zc[tid] / 400.0) * 255.0);
-        float* L = reinterpret_cast<float*>(sm.z_hi);
-#pragma unroll
-        for (int hb = 0; hb < 2; ++hb) {
-#pragma unroll
-          for (int k = 0; k < PPW; ++k) {
-            const int b = 2 * pair[k] + hh;
-            if ((b >> 6) != hb) continue;
-#pragma unroll
-            for (int t = 0; t < NTILE; ++t) {
-              const int f = TF * t + r;
-              if (f < NF) L[(b - 64 * hb) * NF + f] = (fmaxf(dbv[t][k] - ref_db, thr) - d_min) * inv_diff;
-            }
-          }
-          __syncthreads();
-          const int h_lo = 64 * (1 - hb);
-          uint32_t* out = reinterpret_cast<uint32_t*>(a.img + clip * (int64_t)(NMEL * NF * 3) + h_lo * NF * 3);
-          for (int qd = tid; qd < LB / 4; qd += NTH) {
-            uint32_t by[12];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              const int px = 4 * qd + j;
-              const int hr = px / NF, w = px - hr * NF;
-              const double v = (1.0 - (double)L[(63 - hr) * NF + w]) * 255.0;
-              const uint32_t gb = (v >= 0.0) ? ((uint32_t)(int)v & 255u) : 0u;
-              by[3 * j] = sm.rb[w];
-              by[3 * j + 1] = gb;
-              by[3 * j + 2] = gb;
-            }
-#pragma unroll
-            for (int k = 0; k < 3; ++k)
-              out[3 * qd + k] = by[4 * k] | (by[4 * k + 1] << 8) | (by[4 * k + 2] << 16) | (by[4 * k + 3] << 24);
-          }
-          __syncthreads();
-        }
-      }
-    }
-    FE3_MARK(7);
-    FE3_T_STORE(clip)
+    }, std::make_integer_sequence<int, NTILE>{});
   }
 }
 
@@ -1404,15 +1468,15 @@ void od_fe_build_tables(OdFeTables* t) {
         }
   };
   static double A[32][32];
-  for (int n1 = 0; n1 < 16; ++n1) {   // stage 1: rows c = 2 k2 + ri, k = n2; window x W25 x 2^8
+  for (int n1 = 0; n1 < 16; ++n1) {   // stage 1: rows c = 2 k2 + ri, k = n2; window x W25 x 2^9
     for (int i = 0; i < 32; ++i)
       for (int k = 0; k < 32; ++k) A[i][k] = 0.0;
     for (int k2 = 0; k2 < 13; ++k2)
       for (int n2 = 0; n2 < 25; ++n2) {
         const double th = 2.0 * PI * n2 * k2 / 25.0;
         const double w = 0.5 - 0.5 * cos(2.0 * PI * (n1 + 16 * n2) / N_FFT);
-        A[2 * k2][n2] = w * cos(th) * 256.0;
-        A[2 * k2 + 1][n2] = k2 ? -w * sin(th) * 256.0 : 0.0;
+        A[2 * k2][n2] = w * cos(th) * 512.0;
+        A[2 * k2 + 1][n2] = k2 ? -w * sin(th) * 512.0 : 0.0;
       }
     put(t->a1, n1, A);
   }
@@ -1426,7 +1490,7 @@ void od_fe_build_tables(OdFeTables* t) {
       for (int n1 = 0; n1 < 16; ++n1) {
         const double th = 2.0 * PI * n1 * bin / 400.0;
         const double C = cos(th), S = (n1 * bin) % 200 == 0 ? 0.0 : -sin(th);
-        A[2 * i][2 * n1] = C * 128.0;                // re = C a - sg S b  (x 2^7: Z carries 2^1)
+        A[2 * i][2 * n1] = C * 128.0;                // re = C a - sg S b  (x 2^7: Z carries 2^1 of A1's 2^9)
         A[2 * i][2 * n1 + 1] = -sg * S * 128.0;
         A[2 * i + 1][2 * n1] = S * 128.0;            // im = S a + sg C b
         A[2 * i + 1][2 * n1 + 1] = sg * C * 128.0;

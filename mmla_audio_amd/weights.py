@@ -112,7 +112,10 @@ def _orthogonal(rng, shape):
     return q.T
 
 
-def synthetic(kind, seed=0, n_classes=None):
+SI_HEAD_GAIN = 10.0   # synthetic SI Dense kernel scale: decisive argmax at K = 630 (logit std ~4)
+
+
+def synthetic(kind, seed=0, n_classes=None, head_gain=None):
     """Seeded synthetic weights in the reference layout.
 
     Kernels are Glorot-uniform (the Keras default the reference trains from), recurrent kernels
@@ -120,7 +123,10 @@ def synthetic(kind, seed=0, n_classes=None):
     Keras initial (0, 1): they are set from a second-moment estimate propagated through the graph
     so that every BN actually normalises, as a trained model's would, and the stem kernel is scaled
     for the input range (0..255 PNG values for OD, MFCC magnitudes for SI).  All non-zero, so every
-    fused bias / BN / residual term is exercised by parity tests.
+    fused bias / BN / residual term is exercised by parity tests.  The SI head's Dense kernel is
+    scaled by ``head_gain`` (default SI_HEAD_GAIN): Glorot alone gives logits with std ~0.4 over 630
+    classes, a nearly flat softmax a trained classifier would not produce and on which argmax checks
+    decide little.
     """
     rng = np.random.default_rng(np.random.PCG64(0x6D6D6C61 + 7919 * seed + 31 * kind))
     W = {}
@@ -169,6 +175,10 @@ def synthetic(kind, seed=0, n_classes=None):
             continue
         raise AssertionError(f'unexpected role {role} at {name}')
     del resid
+    if head_gain is None:
+        head_gain = SI_HEAD_GAIN if kind == SI else 1.0
+    head = [n for n, _, r in items if r == 'kernel'][-1]
+    W[head] = W[head] * head_gain
     return {k: np.asarray(v, dtype=np.float32) for k, v in W.items()}
 
 

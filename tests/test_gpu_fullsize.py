@@ -1,7 +1,7 @@
 """Full-size batches (BASELINE configs 3 and 4): every clip of a >= 2-micro-batch OD run and a
 65 536-clip SI run equals its batch-1 result, clips are compared at every micro-batch edge (the
 OD activation buffers exceed 2^31 elements there, so a 32-bit index anywhere would show), and a
-sample matches the oracle at the SURVEY 8(d) tolerance with identical argmax.
+sample matches the oracle to |log p - log p_ref| <= 1e-4 with identical argmax (oracle/compare.py).
 
 Inputs are generated in HBM (mmla_audio_amd.synthetic.make_clips) and run through the
 device-pointer ABI like bench.py; the batch-1 references go through the host-pointer ABI.
@@ -9,7 +9,7 @@ device-pointer ABI like bench.py; the batch-1 references go through the host-poi
 import numpy as np
 import pytest
 
-from oracle import nets, od_fe, si_fe
+from oracle import compare, nets, od_fe, si_fe
 
 pytestmark = pytest.mark.gpu
 
@@ -21,11 +21,6 @@ def _sample(n, mb, k_random, seed):
         idx.update((c0, min(c0 + mb, n) - 1))
     idx.update(np.random.default_rng(seed).choice(n, k_random, replace=False).tolist())
     return sorted(idx)
-
-
-def _near_tie(p, tol=1e-4):
-    s = np.sort(p)
-    return s[-1] - s[-2] < tol
 
 
 @pytest.mark.parametrize('prec', ['f16x3', 'f32'])
@@ -53,11 +48,15 @@ def test_od_two_microbatches(prec):
         assert np.array_equal(p1[0], probs[i]) and a1[0] == am[i], f'clip {i} of {n} (mb {mb})'
     if prec == 'f32':
         return
-    for j, i in enumerate(idx[::max(1, len(idx) // 10)]):
-        f = od_fe.od_features(sub[idx.index(i)])
-        ref = nets.od_forward(f['png_rgb'][None].astype(np.float32), W)[0]
-        assert np.abs(probs[i] - ref).max() <= 1e-4, f'clip {i}'
-        assert _near_tie(ref) or am[i] == int(np.argmax(ref)), f'clip {i}'
+    # the network on the kernel's own image: log-probabilities to 1e-4; the argmax on the oracle
+    # front-end's image (which may differ by 1 LSB on a few pixels) except at log-margin near-ties
+    pick = idx[::max(1, len(idx) // 10)]
+    rows = [idx.index(i) for i in pick]
+    img = c.od_features(sub[rows], db=False, norm=False, zcr=False)['img'].astype(np.float32)
+    err = compare.logp_err(probs[pick], nets.od_forward(img, W))
+    assert err <= compare.LOGP_TOL, err
+    ref = nets.od_forward(np.stack([od_fe.od_features(sub[r])['png_rgb'] for r in rows]).astype(np.float32), W)
+    assert compare.argmax_ok(probs[pick], ref)
 
 
 def test_si_65536_clips():
@@ -82,8 +81,10 @@ def test_si_65536_clips():
     c.release_workspace()
     p1, a1, _ = c.si_pipeline(sub)        # a small batch: the same per-clip kernels
     assert np.array_equal(p1, probs) and np.array_equal(a1, am)
-    for j in range(0, len(idx), max(1, len(idx) // 10)):
-        x = si_fe.input_feature_gen(sub[j])
-        ref = nets.si_forward(x.astype(np.float32), W)[0]
-        assert np.abs(probs[j] - ref).max() <= 1e-4, f'clip {idx[j]}'
-        assert _near_tie(ref) or am[j] == int(np.argmax(ref)), f'clip {idx[j]}'
+    rows = list(range(0, len(idx), max(1, len(idx) // 10)))
+    x = np.concatenate([si_fe.input_feature_gen(sub[j]) for j in rows]).astype(np.float32)
+    ref = nets.si_forward(x, W)
+    err = compare.logp_err(probs[rows], ref)
+    assert err <= compare.LOGP_TOL, err
+    assert compare.argmax_ok(probs[rows], ref) and np.array_equal(am[rows], probs[rows].argmax(1))
+    assert compare.near_ties(ref).mean() < 0.05

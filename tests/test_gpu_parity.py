@@ -6,13 +6,14 @@ Tolerances (BASELINE.json north_star):
   OD ZCR                  exact integer crossing counts
   OD image (model input)  R exact; G/B <= 1 LSB on <= 1e-4 of the pixel values of a test
   SI features             max-abs <= 1e-4 on [256, 39] (float64 kernel, float32 store)
-  nets                    probabilities max-abs <= 1e-4 vs a float64 numpy restatement;
-                          argmax identical except near-ties |p_a - p_b| < 1e-4
+  nets                    log-probabilities max |log p - log p_ref| <= 1e-4 vs a float64 numpy
+                          restatement (oracle/compare.py); argmax identical except where the
+                          reference's top-2 log-margin is < 2e-4
 """
 import numpy as np
 import pytest
 
-from oracle import nets, od_fe, si_fe, synth
+from oracle import compare, nets, od_fe, si_fe, synth
 
 pytestmark = pytest.mark.gpu
 
@@ -108,11 +109,14 @@ def test_si_features_sequence_mode(ctx):
 
 
 def _near_tie_ok(p_gpu, p_ref):
-    a = p_gpu.argmax(1)
-    b = p_ref.argmax(1)
-    srt = np.sort(p_ref, axis=1)
-    tie = (srt[:, -1] - srt[:, -2]) < 1e-4
-    return np.all((a == b) | tie)
+    """argmax identical except where the reference's top-2 log-margin is below 2e-4"""
+    return compare.argmax_ok(p_gpu, p_ref)
+
+
+def _logp(p, ref, tol=compare.LOGP_TOL):
+    err = compare.logp_err(p, ref)
+    assert err <= tol, f'max |log p - log p_ref| = {err}'
+    return err
 
 
 def test_od_forward_vs_oracle(ctx, od_golden):
@@ -124,7 +128,7 @@ def test_od_forward_vs_oracle(ctx, od_golden):
                         rng.integers(0, 256, size=(5, 128, 151, 3))]).astype(np.float32)
     p = ctx.od_forward(x)
     ref = nets.od_forward(x, W)
-    assert np.abs(p - ref).max() <= 1e-4, np.abs(p - ref).max()
+    _logp(p, ref)
     assert _near_tie_ok(p, ref)
     p8 = ctx.od_forward(x.astype(np.uint8))
     assert np.array_equal(p8, p)
@@ -140,9 +144,10 @@ def test_si_forward_vs_oracle(ctx, si_golden, k, head):
     p = ctx.si_forward(x.astype(np.float32))
     ref = nets.si_forward(x.astype(np.float32), W, head='softmax' if head == 0 else 'sigmoid')
     assert p.shape == (len(x), k)
-    assert np.abs(p - ref).max() <= 1e-4, np.abs(p - ref).max()
+    _logp(p, ref)
     if k > 1:
         assert _near_tie_ok(p, ref)
+        assert compare.near_ties(ref).mean() < 0.05, 'synthetic head too flat for an argmax check'
 
 
 def test_od_pipeline_matches_features_then_forward(ctx):
@@ -156,11 +161,11 @@ def test_od_pipeline_matches_features_then_forward(ctx):
     assert np.array_equal(probs, p2)
     assert np.array_equal(am, probs.argmax(1))
     ref = nets.od_forward(f['img'].astype(np.float32), W)
-    assert np.abs(probs - ref).max() <= 1e-4
+    _logp(probs, ref)
     # end to end against the oracle front-end too (image may differ by 1 LSB on a few pixels)
     ref_img = np.stack([od_fe.od_features(p)['png_rgb'] for p in pcm]).astype(np.float32)
     ref2 = nets.od_forward(ref_img, W)
-    assert np.abs(probs - ref2).max() <= 1e-3
+    _logp(probs, ref2, 1e-3)
     assert _near_tie_ok(probs, ref2)
 
 
@@ -177,7 +182,7 @@ def test_si_pipeline_silent_and_argmax(ctx):
     x = np.stack([np.zeros((256, 39)) if isinstance(f, str) else f[0] for f in feats]).astype(np.float32)
     ref = nets.si_forward(x, W, head='sigmoid')
     ok = ~silent
-    assert np.abs(probs[ok] - ref[ok]).max() <= 1e-4
+    _logp(probs[ok], ref[ok])
     assert np.array_equal(am[ok], ref[ok].argmax(1))
 
 
@@ -288,7 +293,7 @@ def test_precision_modes_vs_oracle(ctx, prec, si_golden):
         x = np.random.default_rng(12).integers(0, 256, size=(6, 128, 151, 3)).astype(np.float32)
         p = ctx.od_forward(x)
         ref = nets.od_forward(x, W)
-        assert np.abs(p - ref).max() <= 1e-4, (prec, np.abs(p - ref).max())
+        _logp(p, ref)
         for stage in (1, 4, 9, 11):
             got = ctx.debug_od_trace(x[:2], stage)
             want = _oracle_od_stages(x[:2], W)[stage]
@@ -298,6 +303,6 @@ def test_precision_modes_vs_oracle(ctx, prec, si_golden):
         ctx.load_weights(weights.SI, weights.pack(weights.SI, Ws, 630), 630, 0)
         xs = np.stack([si_golden[f'feat_{i}'][0] for i in range(len(si_golden['names']))]).astype(np.float32)
         ps = ctx.si_forward(xs)
-        assert np.abs(ps - nets.si_forward(xs, Ws)).max() <= 1e-4
+        _logp(ps, nets.si_forward(xs, Ws))
     finally:
         ctx.set_precision(_lib.PREC_F16X3)

@@ -1,7 +1,7 @@
 """Per-phase cycles of the MFMA OD front-end (od_fe.hip v3) -- dev tool.
 
 Needs the instrumented library: `make -C mmla_audio_amd/csrc exp` builds libmmla_exp.so with
--DFE_EXP=1 (s_memtime per phase, per wave, summed over the clip's 5 tiles).
+-DFE_EXP=1 (s_memtime per interval of the step pipeline, per wave, summed over a clip's 5 steps).
 Usage: python tools/fe3_timeline.py [waves_per_workgroup=8]
 """
 import ctypes
@@ -24,7 +24,7 @@ buf = (ctypes.c_ulonglong * (4096 * 8))()
 lib.mmla_debug_fe_times(buf)
 nclip = 4096 // nwv
 t = np.frombuffer(buf, dtype=np.uint64).reshape(nclip, nwv, 8).astype(np.float64)
-names = ['stage', 'barrier1', 'zcr+stage1', 'barrier2', 'stage2', 'barrier3', 'mel', 'epilogue']
+names = ['A: s1+mel', 'A barrier', 'B: s2+stage', 'B barrier', 'epilogue', '-', '-', '-']
 tot = t.sum(2)
 print(f'{nwv} waves/workgroup: median cycles per clip (wave 0) {np.median(tot[:, 0]):.0f}, '
       f'max over waves {np.median(tot.max(1)):.0f}')

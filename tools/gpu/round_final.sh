@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-2 final measurement at HEAD: GPU suite, PMC traffic (bench.py reads the committed captures),
+# Round-end measurement at HEAD: GPU suite, PMC traffic (bench.py reads the committed captures),
 # the four bench lines + OD rocprof stats (bench_all.sh), rocprof stats of the SI and FE lines.
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
@@ -8,6 +8,6 @@ timeout -k 10 600 python3 -u -m pytest tests -m gpu -q -x --timeout 300 --timeou
 tail -1 gpurun_out/fin_pytest.log
 bash tools/gpu/pmc_traffic.sh > gpurun_out/pmc_traffic.log 2>&1 || { tail -20 gpurun_out/pmc_traffic.log; exit 1; }
 bash tools/gpu/bench_all.sh || exit $?
-WL=si_pipeline TAG=si BENCH_ARGS="--no-latency" bash tools/gpu/r2_prof.sh || exit $?
-WL=od_features TAG=fe BENCH_ARGS="--no-latency" bash tools/gpu/r2_prof.sh || exit $?
+WL=si_pipeline TAG=si BENCH_ARGS="--no-latency" bash tools/gpu/prof_line.sh || exit $?
+WL=od_features TAG=fe BENCH_ARGS="--no-latency" bash tools/gpu/prof_line.sh || exit $?
 find gpurun_out -type f -size +8M -print -delete; du -sh gpurun_out
