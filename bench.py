@@ -201,14 +201,14 @@ def parity_sample(ctx, wl, pcm, probs, argmax, W, mb, clip_len, k=24):
         out['si_feature_max_abs_err'] = float(np.abs(feat.cpu().numpy() - xs).max())
         ref = Nets(W).si_forward(xs.astype(np.float32))
     if wl in ('od_pipeline', 'si_pipeline'):
+        from oracle import compare
         gp = probs[idx].cpu().numpy()
         ga = argmax[idx].cpu().numpy()
-        srt = np.sort(ref, axis=1)
-        tie = srt[:, -1] - srt[:, -2] < 1e-4
-        agree = ga == np.argmax(ref, axis=1)
-        out.update({'prob_max_abs_err': float(np.abs(gp - ref).max()),
-                    'argmax_agree': int(agree.sum()), 'argmax_disagree_non_tie': int((~agree & ~tie).sum()),
-                    'near_ties': int(tie.sum())})
+        agree, disagree, ties = compare.argmax_report(gp, ref)
+        out.update({'logp_max_abs_err': compare.logp_err(gp, ref), 'prob_max_abs_err': float(np.abs(gp - ref).max()),
+                    'argmax_agree': agree, 'argmax_disagree_non_tie': disagree,
+                    'argmax_matches_probs': bool(np.array_equal(ga, gp.argmax(1))),
+                    'near_ties_log_margin': ties, 'tie_rule': f'top-2 log-margin < {compare.TIE_LOG_MARGIN:g}'})
     return out
 
 

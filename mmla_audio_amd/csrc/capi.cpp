@@ -116,7 +116,8 @@ struct mmla_ctx {
   std::vector<size_t> ws_size;
   std::vector<size_t> ws_guard;   // MMLA_WS_GUARD: guard bytes before and after each slot (0 = none)
   int64_t od_mb = 0, si_mb = 0;            // user caps (0 = sized from free memory)
-  int64_t od_mb_cap = kOdMicrobatch, si_mb_cap = kSiMicrobatch;   // lowered after an OOM retry
+  int64_t od_mb_cap = kOdMicrobatch, si_mb_cap = kSiMicrobatch;   // default caps of the automatic size
+  int debug_fail_allocs = 0;   // test hook (env MMLA_DEBUG_FAIL_ALLOC at create): fail this many workspace allocations
   int precision = MMLA_PREC_F16X3;
   // 3xFP16 range guard: kernels set range_dev[0] (device-pointer calls; sticky until
   // mmla_range_check) or range_dev[1] (host-pointer micro-batches: re-run in exact f32) when an
@@ -235,6 +236,10 @@ int ws_get(mmla_ctx* c, int slot, size_t bytes, void** out) {
       c->ws_size[slot] = 0;
     }
     void* p = nullptr;
+    if (c->debug_fail_allocs > 0) {
+      --c->debug_fail_allocs;
+      return fail(c, MMLA_E_OOM, "workspace slot %d: injected allocation failure (MMLA_DEBUG_FAIL_ALLOC)", slot);
+    }
     if (hipMalloc(&p, bytes + 2 * guard) != hipSuccess) {
       (void)hipGetLastError();   // clear the sticky allocation error
       return fail(c, MMLA_E_OOM, "hipMalloc(%zu) failed for workspace slot %d", bytes, slot);
@@ -499,7 +504,7 @@ int finish(mmla_ctx* c, bool dev) {
 // ---- micro-batching and the 3xFP16 range guard -------------------------------------------------
 
 // clips per micro-batch: the user's cap, else what the device's free memory holds (the slots this
-// context already owns count as free), capped at the default / the cap left by an OOM retry
+// context already owns count as free), capped at the default
 int64_t microbatch(mmla_ctx* c, bool od) {
   const int64_t user = od ? c->od_mb : c->si_mb;
   if (user > 0) return user;
@@ -518,7 +523,8 @@ int64_t microbatch(mmla_ctx* c, bool od) {
 
 // body(c0, cnt) over clips [0, n) in micro-batches.  A workspace allocation failure (MMLA_E_OOM)
 // frees the context's workspaces, halves the micro-batch (unless the caller fixed it with
-// mmla_set_microbatch) and retries the same clips.
+// mmla_set_microbatch) and retries the same clips; the halving holds for the rest of this call only
+// (a transient OOM, e.g. while another context held memory, must not cap every later call).
 template <class F>
 int for_microbatches(mmla_ctx* c, bool od, int64_t n, F&& body) {
   int64_t c0 = 0;
@@ -528,8 +534,7 @@ int for_microbatches(mmla_ctx* c, bool od, int64_t n, F&& body) {
     const int rc = body(c0, cnt);
     if (rc == MMLA_E_OOM && (od ? c->od_mb : c->si_mb) == 0 && cnt > kMinMicrobatch) {
       CHK(ws_release(c));
-      mb = std::max(kMinMicrobatch, cnt / 2);
-      (od ? c->od_mb_cap : c->si_mb_cap) = mb;
+      mb = std::max(kMinMicrobatch, cnt / 2);   // this call only: the next call re-reads free memory
       continue;
     }
     CHK(rc);
@@ -907,6 +912,7 @@ int mmla_create(int device, mmla_ctx** out) {
   if (hipSetDevice(device) != hipSuccess) return MMLA_E_HIP;
   mmla_ctx* c = new mmla_ctx();
   c->device = device;
+  if (const char* fa = std::getenv("MMLA_DEBUG_FAIL_ALLOC")) c->debug_fail_allocs = std::atoi(fa);
   // a BLOCKING stream: it orders with the legacy default (NULL) stream, on which PyTorch's default
   // stream enqueues -- so a device-pointer call sees tensors a torch kernel or copy just produced
   // without an explicit synchronisation (a non-blocking stream raced them: a 65 536-clip call read

@@ -702,7 +702,7 @@ struct Smem {
   uint32_t ztrash[128];                       // stage 1's one unused (k2 = 14) word per lane, hi / lo
   uint32_t t[16 * TP];                        // staged samples, transposed: (hi, lo) fp16 pair of x'[16 q + n1]
   _Float16 z_hi[13 * TF * ZP], z_lo[13 * TF * ZP];   // stage-1 output
-  uint8_t sgn[NCH + 16];                      // per chunk: sign bits of its 8 samples
+  uint8_t sgn[NCH + 16];                      // per chunk c at [c + 1]: sign bits of its 8 samples ([0] = 0)
   uint8_t cnt[NCH + 16];                      // per chunk: crossings (low 4 bits), one into its first sample (bit 4)
   int zc[2][NF + 1];                          // ZCR counts of the clip (double-buffered by clip)
   float red[2][NWV];                          // per-wave max / min of the finished clip's mel power
@@ -739,6 +739,12 @@ MMLA_DEV uint32_t pack_f16(_Float16 a, _Float16 b) {
 MMLA_DEV int s2_bin(int k2, int i) {
   if (k2 == 0) return i <= 8 ? 25 * i : -1;
   return i < 8 ? 25 * i + k2 : 25 * (i - 8) + 25 - k2;
+}
+
+// 10 log10 max(s, 1e-10) as db10, the clamp as one med3 (fmaxf would add a NaN-quieting max;
+// mel sums are never NaN)
+MMLA_DEV float db10m(float s) {
+  return __log2f(__builtin_amdgcn_fmed3f(s, 1e-10f, __builtin_inff())) * 3.0102999566398120f;
 }
 
 // wave-wide max / min through DPP (quad_perm, row_ror) and four readlanes: no lane-index registers
@@ -830,6 +836,7 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
   for (int i = tid; i < 128; i += NTH) sm.mst[i] = tb.mel_start[i] * PP;
   for (int i = tid; i < (PROWS - 201) * PP; i += NTH) sm.p[201 * PP + i] = 0.0f;
   for (int i = tid; i < 16 * (TP - TQS); i += NTH) sm.t[(i / (TP - TQS)) * TP + TQS + i % (TP - TQS)] = 0u;
+  if (tid == 0) sm.sgn[0] = 0;
 
   // an opaque copy of the thread id per use: the tile-unrolled code otherwise hoists every
   // thread-derived address of all tiles out of the clip loop (hundreds of live registers -> spills)
@@ -966,7 +973,7 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
       uint32_t* tq = sm.t + (c & 1) * 8 * TP + (c >> 1);
 #pragma unroll
       for (int j = 0; j < 8; ++j) tq[j * TP] = d[j];
-      sm.sgn[c] = (uint8_t)sg;
+      sm.sgn[c + 1] = (uint8_t)sg;
     }
   };
 
@@ -975,9 +982,11 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
   auto crossings = [&](auto T_) {
     constexpr int t = decltype(T_)::value;
     const int ibase = HOP * TF * t - N_FFT / 2;
-    for (int c = otid(); c < NCH; c += NTH) {
-      const uint32_t m = sm.sgn[c];
-      const uint32_t pv = c > 0 ? (uint32_t)sm.sgn[c - 1] >> 7 : 0u;
+    static_assert(NCH <= NTH, "one chunk per thread");
+    const int c = otid();
+    if (c < NCH) {
+      const uint32_t m = sm.sgn[c + 1];
+      const uint32_t pv = (uint32_t)sm.sgn[c] >> 7;
       uint32_t tr = (m ^ ((m << 1) | pv)) & 0xffu;
       if constexpr (t == 0 || t == NTILE - 1) {
         const int i0 = ibase + 8 * c;
@@ -1129,10 +1138,14 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
       const float* pp = sm.p + sm.mst[b] + r;
       float sacc = 0.0f;
       // taps in batches of 4 (the batch's reads issued before its FMAs): zero weights past the
-      // band's own taps, P rows past bin 200 are zero
+      // band's own taps, P rows past bin 200 are zero.  The tap count is made opaque per use: the
+      // compiler otherwise precomputes all 12 batch conditions of all tiles as SGPR masks, which
+      // spill into VGPR lanes
+      int nt = ptaps[k];
+      asm volatile("" : "+s"(nt));
 #pragma unroll
       for (int j0 = 0; j0 < MW; j0 += 4) {
-        if (j0 >= ptaps[k]) break;
+        if (j0 >= nt) break;
         const float4 w4 = *reinterpret_cast<const float4*>(wp + j0);
         const float p0 = pp[j0 * PP], p1 = pp[(j0 + 1) * PP], p2 = pp[(j0 + 2) * PP], p3 = pp[(j0 + 3) * PP];
         sacc = fmaf(w4.x, p0, sacc);
@@ -1140,7 +1153,7 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
         sacc = fmaf(w4.z, p2, sacc);
         sacc = fmaf(w4.w, p3, sacc);
       }
-      dbv[t][k] = db10(sacc);
+      dbv[t][k] = db10m(sacc);
       if (TF * t + TF <= NF || TF * t + r < NF) {
         smax = fmaxf(smax, sacc);
         smin = fminf(smin, sacc);
@@ -1159,10 +1172,13 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
       mx = fmaxf(mx, sm.red[0][w]);
       mn = fminf(mn, sm.red[1][w]);
     }
-    const float ref_db = (float)(10.0 * log10(fmax(1e-10, (double)mx)));
-    const float d_max = db10(mx) - ref_db;
+    // ref = np.max: numpy takes 10 log10 of the float32 max in float64 and subtracts it in float32;
+    // the kernel's own db10 of the max is within an ulp of that and makes d_max exactly 0 (the shift
+    // cancels in the normalisation; the dB outputs move by ~1e-5 dB, tolerance 5e-3)
+    const float ref_db = db10m(mx);
+    const float d_max = db10m(mx) - ref_db;
     const float thr = d_max - 80.0f;
-    const float d_min = fmaxf(db10(mn) - ref_db, thr);
+    const float d_min = fmaxf(db10m(mn) - ref_db, thr);
     const float diff = d_max - d_min;
     const float inv_diff = 1.0f / diff;
     const int tz = otid();

@@ -519,7 +519,10 @@ def _odpost_case(ofg_mod, tmp):
     return out
 
 
-def main(parts=('od', 'si', 'seg', 'exp', 'vad', 'sipost', 'odpost')):
+N_PNG_BYTES = 4
+
+
+def main(parts=('od', 'si', 'seg', 'exp', 'vad', 'sipost', 'odpost', 'odpng')):
     _install_stubs()
     ofg_mod = _load_reference('OverlapDetection/scripts/overlap_features_generator.py', 'ref_ofg')
     si_mod = _load_reference('SpeakerIdentification/scripts/speaker_identification.py', 'ref_si')
@@ -527,6 +530,20 @@ def main(parts=('od', 'si', 'seg', 'exp', 'vad', 'sipost', 'odpost')):
     assert ofg.get_attributes() == (400, 160, 16000)
 
     tmp = tempfile.mkdtemp(prefix='mmla_golden_')
+    if 'odpng' in parts:
+        # the PNG files the reference's own generate_zcr_image -> plt.imsave(origin='lower') wrote
+        # (real matplotlib), byte for byte, for the first OD cases
+        png = {'names': np.array([c[0] for c in OD_CASES[:N_PNG_BYTES]])}
+        for i, (name, gen) in enumerate(OD_CASES[:N_PNG_BYTES]):
+            wav = os.path.join(tmp, f'odpng{i}.wav')
+            _write_wav(wav, gen())
+            ofg.generate_zcr_image(wav, tmp + '/', f'odpng{i}.png')
+            with open(os.path.join(tmp, f'odpng{i}.png'), 'rb') as f:
+                png[f'bytes_{i}'] = np.frombuffer(f.read(), np.uint8)
+            print('PNG', name, png[f'bytes_{i}'].size, 'bytes')
+        np.savez_compressed(os.path.join(HERE, 'od_png_golden.npz'), **png)
+        if parts == ('odpng',):
+            return
     if 'odpost' in parts:
         np.savez_compressed(os.path.join(HERE, 'odpost_golden.npz'), **_odpost_case(ofg_mod, tmp))
         if parts == ('odpost',):
@@ -583,4 +600,4 @@ def main(parts=('od', 'si', 'seg', 'exp', 'vad', 'sipost', 'odpost')):
 
 
 if __name__ == '__main__':
-    main(tuple(sys.argv[1:]) or ('od', 'si', 'seg', 'exp', 'vad', 'sipost', 'odpost'))
+    main(tuple(sys.argv[1:]) or ('od', 'si', 'seg', 'exp', 'vad', 'sipost', 'odpost', 'odpng'))

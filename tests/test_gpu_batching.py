@@ -79,3 +79,26 @@ def test_od_silent_gate(ctx):
     # without lens the clip length decides for every clip
     _, a2, s2 = ctx.od_pipeline(np.zeros((3, 3000), np.int16))
     assert s2.all() and (a2 == -1).all()
+
+
+def test_oom_retry_halves_this_call_only(monkeypatch):
+    """a workspace OOM halves the micro-batch for the rest of that call and nothing
+    else -- the next call is sized from free memory again (MMLA_DEBUG_FAIL_ALLOC=1 injects one
+    allocation failure into a fresh context)."""
+    from mmla_audio_amd import _lib, weights
+    W = weights.synthetic(weights.OD, seed=21)
+    pcm = synth.batch(950, 150, 40000)
+    ref = _lib.Context(0)
+    ref.load_weights(weights.OD, weights.pack(weights.OD, W), 2)
+    p_ref, a_ref, _ = ref.od_pipeline(pcm)
+    monkeypatch.setenv('MMLA_DEBUG_FAIL_ALLOC', '1')
+    c = _lib.Context(0)
+    monkeypatch.delenv('MMLA_DEBUG_FAIL_ALLOC')
+    c.load_weights(weights.OD, weights.pack(weights.OD, W), 2)
+    mb0 = c.get_microbatch()[0]
+    assert mb0 >= 150
+    p, a, _ = c.od_pipeline(pcm)        # first workspace allocation fails -> 75 + 75
+    assert np.array_equal(p, p_ref) and np.array_equal(a, a_ref)
+    assert c.get_microbatch()[0] == mb0  # not capped at 75 for later calls
+    p2, _, _ = c.od_pipeline(pcm)
+    assert np.array_equal(p2, p_ref)

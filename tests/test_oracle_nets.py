@@ -35,3 +35,33 @@ def test_keras_same_padding():
     assert y[0, :, 0, 0].tolist() == [0, 0, 1, 2, 3]
     mp = nets.maxpool2d_same(np.arange(1, 4, dtype=np.float64).reshape(1, 1, 3, 1))
     assert mp.ravel().tolist() == [2, 3]
+
+
+def test_si_k630_log_prob_bar_catches_a_1e3_logit_perturbation(si_golden):
+    """the SI K = 630 parity bar (|log p_gpu - log p_ref| <= 1e-4, oracle/compare.py)
+    must FAIL when the logits are off by 1e-3 relative -- checked here on the CPU oracle itself, with
+    the inputs of tests/test_gpu_parity.py::test_si_forward_vs_oracle (the synthetic head's scale makes
+    the argmax decisive: ties by log-margin < 5 %)."""
+    from oracle import compare
+    W = weights.synthetic(weights.SI, seed=2, n_classes=630)
+    x = np.stack([si_golden[f'feat_{i}'][0] for i in range(len(si_golden['names']))])
+    x = np.concatenate([x, np.random.default_rng(5).standard_normal((9, 256, 39)) * 10]).astype(np.float32)
+    z = nets.si_forward(x, W, return_logits=True)
+    p = nets.softmax(z)
+    assert compare.logp_err(nets.softmax(z * (1 + 1e-3)), p) > compare.LOGP_TOL
+    assert compare.logp_err(nets.softmax(z * (1 - 1e-3)), p) > compare.LOGP_TOL
+    # one class's logit alone, 1e-3 relative: caught too (for the clip's top class)
+    zz = z.copy()
+    top = zz.argmax(1)
+    zz[np.arange(len(zz)), top] *= 1 + 1e-3
+    assert compare.logp_err(nets.softmax(zz), p) > compare.LOGP_TOL
+    # with the unscaled Glorot head (round 2's synthetic weights) an absolute 1e-4 probability bar
+    # passed this perturbation: the flat 630-way softmax moves each p by < 1e-5
+    W1 = weights.synthetic(weights.SI, seed=2, n_classes=630, head_gain=1.0)
+    z1 = nets.si_forward(x, W1, return_logits=True)
+    p1 = nets.softmax(z1)
+    assert np.abs(nets.softmax(z1 * (1 + 1e-3)) - p1).max() < 1e-4
+    assert compare.logp_err(nets.softmax(z1 * (1 + 1e-3)), p1) > compare.LOGP_TOL
+    assert compare.near_ties(p).mean() < 0.05
+    # and the float32 restatement (what a correct GPU run differs by) stays inside the bar
+    assert compare.logp_err(nets.si_forward(x, W, dtype=np.float32), p) <= compare.LOGP_TOL
