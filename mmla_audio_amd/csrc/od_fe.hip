@@ -845,6 +845,11 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
     asm volatile("" : "+v"(v));
     return v;
   };
+  // the staging thread order starts at wave SW0: waves 13..15 (no stage-2 GEMM) take the first 192
+  // chunks, so interval B's staging lands mostly on the waves stage 2 leaves idle
+  constexpr int SW0 = 13;
+  auto stid = [&]() { return (otid() + (NWV - SW0) * 64) & (NTH - 1); };
+  static_assert(NWV == 16, "staging order assumes 16 waves");
 
   // clip facts the staging needs, wave-uniform
   struct ClipIn {
@@ -872,7 +877,7 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
     if (clip_ >= n_clips) return;
     const ClipIn ci = clip_in(clip_);
     if (!ci.fast) return;
-    const int c = otid() - (t == NTILE - 1 ? ROT4 : 0);
+    const int c = stid() - (t == NTILE - 1 ? ROT4 : 0);
     const int i0 = HOP * TF * t - N_FFT / 2 + 8 * c;
     if (c >= 0 && c < NCH && i0 >= 0 && i0 + 8 <= ci.len) {
       const uint4 v = *reinterpret_cast<const uint4*>(ci.src + i0);
@@ -889,7 +894,7 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
     constexpr int t = decltype(T_)::value;
     if constexpr (FE3_SKIP & 1) return;
     const ClipIn ci = clip_in(clip);
-    const int c = otid() - (t == NTILE - 1 ? ROT4 : 0);
+    const int c = stid() - (t == NTILE - 1 ? ROT4 : 0);
     const int i0 = HOP * TF * t - N_FFT / 2 + 8 * c;
     const bool live = c >= 0 && c < NCH;
     uint32_t d[8];               // (hi, lo) of x' = x 2^-12 (int16 PCM) or y 2^3 (float PCM, y = x / 32768)
@@ -928,9 +933,10 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
       // 465..489) take their samples from the chunks they mirror, lanes of the same wave:
       //   tile 0: p' = 400 - p  -> chunk 49 - c elements 8 - j (j >= 1), chunk 50 - c element 0
       //   tile 4: p' = 7438 - p -> chunk 929 - c elements 6 - j (j <= 6), chunk 928 - c element 7
+      // (staging wave = (first ? 0 : (465 + ROT4) / 64) in the staging order, i.e. that + SW0 mod 16)
       if constexpr (t == 0 || t == NTILE - 1) {
         constexpr bool first = t == 0;
-        if (wid == (first ? 0 : (465 + ROT4) / 64)) {
+        if (wid == ((first ? 0 : (465 + ROT4) / 64) + SW0) % NWV) {
           const int pa = first ? 49 - c : 929 - c, pb = first ? 50 - c : 928 - c;
           const int la = (pa + (first ? 0 : ROT4)) & 63, lb = (pb + (first ? 0 : ROT4)) & 63;
           uint32_t ma[4], mb;
@@ -1137,21 +1143,35 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
       const float* wp = sm.mw + b * MW;
       const float* pp = sm.p + sm.mst[b] + r;
       float sacc = 0.0f;
-      // taps in batches of 4 (the batch's reads issued before its FMAs): zero weights past the
-      // band's own taps, P rows past bin 200 are zero.  The tap count is made opaque per use: the
-      // compiler otherwise precomputes all 12 batch conditions of all tiles as SGPR masks, which
-      // spill into VGPR lanes
+      // taps in batches of 1, 1, 2, 4, 4 (a batch's reads issued before its FMAs): a pair runs the
+      // batches up to its (wave-uniform) tap count, so the 1-2-tap low bands read 1-2 taps instead of
+      // a padded 4 (Slaney 128 x 201: 552 -> 464 tap reads per frame over all bands, was 688 with
+      // batches of 4); zero weights past a band's own taps, P rows past bin 200 are zero.  The tap
+      // count is made opaque per use: the compiler otherwise precomputes all batch conditions of all
+      // tiles as SGPR masks, which spill into VGPR lanes
       int nt = ptaps[k];
       asm volatile("" : "+s"(nt));
+      constexpr int BLO[5] = {0, 1, 2, 4, 8}, BN[5] = {1, 1, 2, 4, 4};
 #pragma unroll
-      for (int j0 = 0; j0 < MW; j0 += 4) {
+      for (int bi = 0; bi < 5; ++bi) {
+        const int j0 = BLO[bi];
         if (j0 >= nt) break;
-        const float4 w4 = *reinterpret_cast<const float4*>(wp + j0);
-        const float p0 = pp[j0 * PP], p1 = pp[(j0 + 1) * PP], p2 = pp[(j0 + 2) * PP], p3 = pp[(j0 + 3) * PP];
-        sacc = fmaf(w4.x, p0, sacc);
-        sacc = fmaf(w4.y, p1, sacc);
-        sacc = fmaf(w4.z, p2, sacc);
-        sacc = fmaf(w4.w, p3, sacc);
+        if constexpr (true) {
+          float wv[4], pv[4];
+          if (BN[bi] == 4) {
+            const float4 w4 = *reinterpret_cast<const float4*>(wp + j0);
+            wv[0] = w4.x; wv[1] = w4.y; wv[2] = w4.z; wv[3] = w4.w;
+          } else if (BN[bi] == 2) {
+            const float2 w2 = *reinterpret_cast<const float2*>(wp + j0);
+            wv[0] = w2.x; wv[1] = w2.y;
+          } else {
+            wv[0] = wp[j0];
+          }
+#pragma unroll
+          for (int j = 0; j < BN[bi]; ++j) pv[j] = pp[(j0 + j) * PP];
+#pragma unroll
+          for (int j = 0; j < BN[bi]; ++j) sacc = fmaf(wv[j], pv[j], sacc);
+        }
       }
       dbv[t][k] = db10m(sacc);
       if (TF * t + TF <= NF || TF * t + r < NF) {
