@@ -1143,35 +1143,22 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
       const float* wp = sm.mw + b * MW;
       const float* pp = sm.p + sm.mst[b] + r;
       float sacc = 0.0f;
-      // taps in batches of 1, 1, 2, 4, 4 (a batch's reads issued before its FMAs): a pair runs the
-      // batches up to its (wave-uniform) tap count, so the 1-2-tap low bands read 1-2 taps instead of
-      // a padded 4 (Slaney 128 x 201: 552 -> 464 tap reads per frame over all bands, was 688 with
-      // batches of 4); zero weights past a band's own taps, P rows past bin 200 are zero.  The tap
-      // count is made opaque per use: the compiler otherwise precomputes all batch conditions of all
-      // tiles as SGPR masks, which spill into VGPR lanes
+      // taps in batches of 4 (the batch's reads issued before its FMAs): zero weights past the
+      // band's own taps, P rows past bin 200 are zero.  (Batches of 1, 1, 2, 4, 4 read 33 % fewer
+      // taps but cost more LDS round trips: the interval got 9 % longer.)  The tap count is made
+      // opaque per use: the compiler otherwise precomputes all batch conditions of all tiles as SGPR
+      // masks, which spill into VGPR lanes
       int nt = ptaps[k];
       asm volatile("" : "+s"(nt));
-      constexpr int BLO[5] = {0, 1, 2, 4, 8}, BN[5] = {1, 1, 2, 4, 4};
 #pragma unroll
-      for (int bi = 0; bi < 5; ++bi) {
-        const int j0 = BLO[bi];
+      for (int j0 = 0; j0 < MW; j0 += 4) {
         if (j0 >= nt) break;
-        if constexpr (true) {
-          float wv[4], pv[4];
-          if (BN[bi] == 4) {
-            const float4 w4 = *reinterpret_cast<const float4*>(wp + j0);
-            wv[0] = w4.x; wv[1] = w4.y; wv[2] = w4.z; wv[3] = w4.w;
-          } else if (BN[bi] == 2) {
-            const float2 w2 = *reinterpret_cast<const float2*>(wp + j0);
-            wv[0] = w2.x; wv[1] = w2.y;
-          } else {
-            wv[0] = wp[j0];
-          }
-#pragma unroll
-          for (int j = 0; j < BN[bi]; ++j) pv[j] = pp[(j0 + j) * PP];
-#pragma unroll
-          for (int j = 0; j < BN[bi]; ++j) sacc = fmaf(wv[j], pv[j], sacc);
-        }
+        const float4 w4 = *reinterpret_cast<const float4*>(wp + j0);
+        const float p0 = pp[j0 * PP], p1 = pp[(j0 + 1) * PP], p2 = pp[(j0 + 2) * PP], p3 = pp[(j0 + 3) * PP];
+        sacc = fmaf(w4.x, p0, sacc);
+        sacc = fmaf(w4.y, p1, sacc);
+        sacc = fmaf(w4.z, p2, sacc);
+        sacc = fmaf(w4.w, p3, sacc);
       }
       dbv[t][k] = db10m(sacc);
       if (TF * t + TF <= NF || TF * t + r < NF) {
