@@ -666,6 +666,9 @@ typedef uint16_t us2 __attribute__((ext_vector_type(2)));
 #ifndef FE3_NWV
 #define FE3_NWV 16
 #endif
+#ifndef FE3_PRIO
+#define FE3_PRIO 0
+#endif
 #ifndef FE3_SKIP
 #define FE3_SKIP 0   // dev timing builds only: 1 staging, 2 stage 1, 4 stage 2, 8 mel, 16 norm stores skipped
 #endif
@@ -677,7 +680,9 @@ constexpr int TQ = 344;                       // q columns of T: p = 16 q + n1; 
 constexpr int TQS = 335;                      //   q 335..343 (only multiplied by zero A1 columns) zeroed once
 constexpr int TP = 346;                       // T row pitch (dwords, even: 8-B reads; rows 8 apart 16 banks apart)
 constexpr int NCH = TQS * 16 / 8;             // 670 chunks of 8 samples staged per tile
-constexpr int ZP = 40;                        // Z row pitch (halves): conflict-free 16-B reads
+constexpr int ZP = 36;                        // Z row pitch (halves): 18 dwords -- stage 1's dword stores
+                                              // of 32 frame rows 2-way (free; 40 was 4-way, ~6 k LDS
+                                              // conflict cycles per clip), stage 2's 8-B reads conflict-free
 constexpr int PP = 34;                        // P row pitch (floats)
 constexpr int PROWS = 212;                    // bins 0..200 + zero rows read by the last mel taps
 constexpr int PTRASH = PROWS;                 // + one row that stage 2's unused lanes write
@@ -1071,13 +1076,15 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
     for (int j = 0; j < G2; ++j) {
       const int k2 = wid + NWV * j;
       if (k2 >= 13 || (FE3_SKIP & 4)) continue;
-      const _Float16* zh = sm.z_hi + (k2 * TF + r) * ZP + 8 * hh;
-      const _Float16* zl = sm.z_lo + (k2 * TF + r) * ZP + 8 * hh;
+      const uint2* zh = reinterpret_cast<const uint2*>(sm.z_hi + (k2 * TF + r) * ZP + 8 * hh);
+      const uint2* zl = reinterpret_cast<const uint2*>(sm.z_lo + (k2 * TF + r) * ZP + 8 * hh);
       f32x16 acc = {};
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        const f16x8 BH = *reinterpret_cast<const f16x8*>(zh + 16 * s);
-        const f16x8 BL = *reinterpret_cast<const f16x8*>(zl + 16 * s);
+        // the fragment's 16 B as two 8-B reads (rows are 8-B, not 16-B, aligned)
+        const uint2 h0 = zh[4 * s], h1 = zh[4 * s + 1], l0 = zl[4 * s], l1 = zl[4 * s + 1];
+        const f16x8 BH = __builtin_bit_cast(f16x8, uint4{h0.x, h0.y, h1.x, h1.y});
+        const f16x8 BL = __builtin_bit_cast(f16x8, uint4{l0.x, l0.y, l1.x, l1.y});
         acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a2l[j][s], BH, acc, 0, 0, 0);
         acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a2h[j][s], BL, acc, 0, 0, 0);
         acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a2h[j][s], BH, acc, 0, 0, 0);
@@ -1222,6 +1229,13 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
   };
 
   const int64_t my_clips = (int64_t)blockIdx.x < n_clips ? (n_clips - 1 - blockIdx.x) / gridDim.x + 1 : 0;
+#if FE3_PRIO
+  // static issue priority by dispatch age (the SIMD's four waves are wid, wid + 4, wid + 8, wid + 12):
+  // the youngest, the arbitration losers that end every barrier interval, go first
+  if (wid >= 12) __builtin_amdgcn_s_setprio(3);
+  else if (wid >= 8) __builtin_amdgcn_s_setprio(2);
+  else if (wid >= 4) __builtin_amdgcn_s_setprio(1);
+#endif
   FE3_T_INIT
   if (my_clips > 0) {
     prefetch(blockIdx.x, tile_c<0>{});

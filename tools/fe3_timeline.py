@@ -15,7 +15,7 @@ from mmla_audio_amd import _lib  # noqa: E402
 from oracle import synth  # noqa: E402
 
 nwv = int(sys.argv[1]) if len(sys.argv) > 1 else 8
-lib = _lib.load_library(os.path.join(os.path.dirname(_lib.LIB_PATH), 'libmmla_exp.so'))
+lib = _lib.load_library(os.environ.get('FE3_LIB', os.path.join(os.path.dirname(_lib.LIB_PATH), 'libmmla_exp.so')))
 ctx = _lib.Context(0)
 pcm = synth.batch(0, 4096, 40000)
 for _ in range(3):
