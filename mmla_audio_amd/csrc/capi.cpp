@@ -348,7 +348,8 @@ int take_conv(mmla_ctx* c, Cursor& cur, std::vector<void*>& al, int kh, int kw, 
   CHK(upload(c, al, bp.data(), bp.size() * sizeof(float), &w->bias));
   // spatial conv: also the 3xFP16 operand layout (cin % 4 != 0: only the SI stem's 4-tap Conv1D,
   // conv_h3.hip stages it element-wise)
-  if (kh * kw > 1 && (cin % 4 == 0 || (kh == 4 && kw == 1 && cout <= 32))) {
+  // (1x1 convs with 16-channel steps too: the OD pool blocks' shortcut, fused into the pooled conv(4,1))
+  if ((kh * kw > 1 && (cin % 4 == 0 || (kh == 4 && kw == 1 && cout <= 32))) || (kh * kw == 1 && cin % 16 == 0)) {
     w->cin_pad = (cin + 15) / 16 * 16;
     const size_t n = (size_t)kh * kw * w->cout_pad * w->cin_pad;
     std::vector<uint16_t> hi(n), lo(n);
@@ -624,11 +625,22 @@ int conv_run(mmla_ctx* c, const ConvArgs& a, int stage = MMLA_STAGE_CONV) {
 
 // spatial conv on the 3xFP16 path when enabled (falls back to the exact-f32 kernel otherwise);
 // pool_out: write MaxPool2D(2,'same') of the output instead of the output (OD pool blocks).
+// sc / sc_x (pool_out only): the block's shortcut Conv2D(1x1, stride 2) of sc_x, added to the pooled
+// output inside the same launch
 int conv_spatial(mmla_ctx* c, const ConvW& w, const float* x, float* y, int n, int h, int wd,
                  const BnW* bn, int pro, int epi, const float* res, bool pool_out = false,
-                 int pool_in_h = 0) {
+                 int pool_in_h = 0, const ConvW* sc = nullptr, const float* sc_x = nullptr) {
   if (c->precision == MMLA_PREC_F16X3 && w.wh) {
     ConvH3Args a{};
+    double sc_flops = 0.0;
+    if (sc && sc_x) {
+      a.sc_x = sc_x;
+      a.sc_wh = sc->wh;
+      a.sc_wl = sc->wl;
+      a.sc_bias = sc->bias;
+      a.sc_cin = sc->cin;
+      sc_flops = 2.0 * n * ((h + 1) / 2) * ((wd + 1) / 2) * sc->cin * sc->cout;
+    }
     a.pool_in = pool_in_h > 0;   // x = the unpooled [n, pool_in_h, 1, cin] (MaxPool1D fused)
     a.h_in = pool_in_h;
     a.x = x;
@@ -654,7 +666,7 @@ int conv_spatial(mmla_ctx* c, const ConvW& w, const float* x, float* y, int n, i
     a.epi = epi;
     a.pool_out = pool_out ? 1 : 0;
     a.range_flag = c->range_ptr;
-    LAUNCH(c, MMLA_STAGE_CONV, 2.0 * n * h * wd * w.kh * w.kw * w.cin * w.cout,
+    LAUNCH(c, MMLA_STAGE_CONV, 2.0 * n * h * wd * w.kh * w.kw * w.cin * w.cout + sc_flops,
            conv_h3_launch(a, c->stream));
     return MMLA_OK;
   }
@@ -770,11 +782,18 @@ int run_od_net(mmla_ctx* c, const uint8_t* img_u8, const float* img_f32, int64_t
     CHK(conv_spatial(c, B.c3, X, T1, (int)n, h, w, &B.bn_in, PRO_BN_ELU, EPI_BIAS, nullptr));
     if (POOL[b]) {
       if (c->precision == MMLA_PREC_F16X3) {
-        // conv(4,1) with MaxPool2D(2,'same') fused into its epilogue -> T2 at half resolution;
-        // then shortcut Conv2D(1x1, stride 2) + pooled T2
-        CHK(conv_spatial(c, B.c4, T1, T2, (int)n, h, w, &B.bn_mid, PRO_BN_ELU, EPI_BIAS, nullptr,
-                         true));
-        CHK(conv_run(c, conv_args(B.sc, X, T1, (int)n, h, w, 2, nullptr, PRO_NONE, EPI_ADD, T2)));
+        if (B.sc.wh && B.sc.cout == B.c4.cout && B.c4.cout_pad == B.sc.cout_pad) {
+          // conv(4,1) + MaxPool2D(2,'same') + the shortcut Conv2D(1x1, stride 2) of X + Add, one launch
+          CHK(conv_spatial(c, B.c4, T1, T2, (int)n, h, w, &B.bn_mid, PRO_BN_ELU, EPI_BIAS, nullptr,
+                           true, 0, &B.sc, X));
+          std::swap(T1, T2);
+        } else {
+          // conv(4,1) with MaxPool2D(2,'same') fused into its epilogue -> T2 at half resolution;
+          // then shortcut Conv2D(1x1, stride 2) + pooled T2
+          CHK(conv_spatial(c, B.c4, T1, T2, (int)n, h, w, &B.bn_mid, PRO_BN_ELU, EPI_BIAS, nullptr,
+                           true));
+          CHK(conv_run(c, conv_args(B.sc, X, T1, (int)n, h, w, 2, nullptr, PRO_NONE, EPI_ADD, T2)));
+        }
       } else {
         CHK(conv_spatial(c, B.c4, T1, T2, (int)n, h, w, &B.bn_mid, PRO_BN_ELU, EPI_BIAS, nullptr));
         // shortcut Conv2D(1x1, stride 2) + MaxPool2D(2, 'same')(t2), fused

@@ -503,6 +503,57 @@ __global__ void __launch_bounds__(NT, (conv_minw<KH, BN, TW, EPI, SHP::FIXED>())
   } else {
   // lane's accumulator register r holds tile row m = mbase + (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
   const int hsel = 4 * (lane >> 5);
+  // pooled blocks: the shortcut Conv2D(1x1, stride 2) as a 3xFP16 GEMM whose accumulator layout is
+  // the pooled one.  A lane's pooled outputs are (m-tile mt, window j) = 4 per m-tile, 16 in all --
+  // one 32x32 MFMA tile: register r = 4 mt + j of lane-half h is row (r & 3) + 8 (r >> 2) + 4 h, so A
+  // row rho holds the input pixel of window (mt = rho >> 3, j = rho & 3, h = (rho >> 2) & 1), i.e. the
+  // window's top-left pixel (oh, ow) -- exactly the pixel the stride-2 1x1 conv samples
+  f32x16 sacc[NTL];
+  bool has_sc = false;
+  if constexpr (POOL && MT == 4) {   // other tilings: the launcher refuses a shortcut
+    has_sc = a.sc_x != nullptr;
+    if (has_sc) {
+      constexpr int TWP = TW == 16 ? 16 : 8;
+      const int rho = lane & 31;
+      const int smt = rho >> 3, sj = rho & 3, sh = (rho >> 2) & 1;
+      // the j-th (q, e) window of the pooled loop below: TW 16 -> q = j >> 1; TW 8 -> q = 2 (j >> 1)
+      const int sq = TW == 16 ? (sj >> 1) : 2 * (sj >> 1), se = 2 * (sj & 1);
+      const int sm_ = (wm * MT + smt) * 32 + 8 * sq + 4 * sh + se;
+      const int soh = h0 + sm_ / TWP, sow = w0 + sm_ % TWP;
+      const bool sok = soh < A_H && sow < A_W;
+      const float* sx = a.sc_x + ((clip * A_H + (sok ? soh : 0)) * A_W + (sok ? sow : 0)) * a.sc_cin + koff;
+      const size_t sks = (size_t)(A_COUTP / 32) * 512;
+#pragma unroll
+      for (int nt = 0; nt < NTL; ++nt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) sacc[nt][i] = 0.0f;
+      for (int s = 0; s < a.sc_cin / 16; ++s) {
+        float4 x0 = make_float4(0.f, 0.f, 0.f, 0.f), x1 = x0;
+        if (sok) {
+          x0 = *reinterpret_cast<const float4*>(sx + 16 * s);
+          x1 = *reinterpret_cast<const float4*>(sx + 16 * s + 4);
+        }
+        const float xv[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+        f16x8 xh, xl;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          rbad |= !(fabsf(xv[k]) < ACT_RANGE);
+          const float v = xv[k] * ACT_SCALE;
+          xh[k] = (_Float16)v;
+          xl[k] = (_Float16)(v - (float)xh[k]);
+        }
+#pragma unroll
+        for (int nt = 0; nt < NTL; ++nt) {
+          const size_t u = (size_t)s * sks + lofs[nt];
+          const f16x8 wh = *reinterpret_cast<const f16x8*>(a.sc_wh + u);
+          const f16x8 wl = *reinterpret_cast<const f16x8*>(a.sc_wl + u);
+          sacc[nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(xh, wl, sacc[nt], 0, 0, 0);
+          sacc[nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(xl, wh, sacc[nt], 0, 0, 0);
+          sacc[nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(xh, wh, sacc[nt], 0, 0, 0);
+        }
+      }
+    }
+  }
   // the residual is added in place (res == y): all of the lane's residual loads are issued before
   // its first store, otherwise every load waits behind the previous (possibly aliasing) store
   float rsd[NTL][MT][16];
@@ -552,6 +603,7 @@ __global__ void __launch_bounds__(NT, (conv_minw<KH, BN, TW, EPI, SHP::FIXED>())
         static_assert(TW == 16 || TW == 8, "pooled epilogue needs TW 8 or 16");
         constexpr int TWP = TW == 16 ? 16 : 8;
         const int hp = (A_H + 1) >> 1, wp = (A_W + 1) >> 1;
+        const float bsc = has_sc ? a.sc_bias[co] : 0.0f;
 #pragma unroll
         for (int q = 0; q < 4; ++q)
 #pragma unroll
@@ -560,6 +612,9 @@ __global__ void __launch_bounds__(NT, (conv_minw<KH, BN, TW, EPI, SHP::FIXED>())
             const int i = 8 * q + hsel + e;
             if ((i / TWP) & 1) continue;                   // only top rows of window pairs
             if (4 * q + e + R + 1 > 15) continue;
+            // window index j of this m-tile (the shortcut accumulator's register 4 mt + j): the rows
+            // kept above depend on q only (hsel + e < 8), so j is compile-time
+            const int jr = TW == 16 ? 2 * q + e / 2 : (q >> 1) * 2 + e / 2;
             const int m = mbase + i;
             const int oh = h0 + m / TWP, ow = w0 + m % TWP;
             if (oh >= A_H || ow >= A_W) continue;
@@ -569,6 +624,8 @@ __global__ void __launch_bounds__(NT, (conv_minw<KH, BN, TW, EPI, SHP::FIXED>())
               mx = fmaxf(mx, v[4 * q + e + R]);
               if (ow + 1 < A_W) mx = fmaxf(mx, v[4 * q + e + R + 1]);
             }
+            // Add()([MaxPool2D(t2), shortcut]): the shortcut's bias added in its own rounding step
+            if (has_sc) mx += fmaf(sacc[nt][4 * mt + jr], UNSCALE, bsc);
             a.y[((clip * hp + (oh >> 1)) * wp + (ow >> 1)) * A_COUT + co] = mx;
           }
       } else {
@@ -629,6 +686,9 @@ template <int KH, int KW, int CK, int BN, int TW, int PRO, int EPI, bool POOL, b
           bool PIN = false, class SHP = Shape<0, 0, 0, 0>>
 hipError_t launch(ConvH3Args a, hipStream_t s) {
   constexpr int BMK = tile_px<KH, BN, TW>();
+  // the fused pooled shortcut needs 4 m-tiles per wave (16 pooled outputs per lane) and 16-channel steps
+  constexpr int WN_ = BN / 32, MT_ = BMK / ((4 / WN_) * 32);
+  if (a.sc_x && (!POOL || MT_ != 4 || a.sc_cin % 16 != 0 || a.sc_cin <= 0)) return hipErrorInvalidValue;
   if constexpr (TW == 0) {
     a.th = 0;
     a.tiles_w = 1;

@@ -204,7 +204,7 @@ def test_si_post_detector_state_carries_across_conversations(ctx):
         def predict(self, x):
             return np.full((len(x), 2), 0.5)
 
-    convs = [[_clip(60 + 2 * c + k, 40960) for k in range(2)] for c in range(2)]
+    convs = [[_clip(76 + 2 * c + k, 40960) for k in range(2)] for c in range(2)]
     ref = webrtc_vad.Vad(3)
     want = [[i for i, s in enumerate(segs) if len(ovad.remove_silence(s, ref.is_speech)[0]) < 4000]
             for segs in convs]
