@@ -629,7 +629,8 @@ int conv_run(mmla_ctx* c, const ConvArgs& a, int stage = MMLA_STAGE_CONV) {
 // output inside the same launch
 int conv_spatial(mmla_ctx* c, const ConvW& w, const float* x, float* y, int n, int h, int wd,
                  const BnW* bn, int pro, int epi, const float* res, bool pool_out = false,
-                 int pool_in_h = 0, const ConvW* sc = nullptr, const float* sc_x = nullptr) {
+                 int pool_in_h = 0, const ConvW* sc = nullptr, const float* sc_x = nullptr,
+                 int sc_h = 0) {
   if (c->precision == MMLA_PREC_F16X3 && w.wh) {
     ConvH3Args a{};
     double sc_flops = 0.0;
@@ -639,7 +640,10 @@ int conv_spatial(mmla_ctx* c, const ConvW& w, const float* x, float* y, int n, i
       a.sc_wl = sc->wl;
       a.sc_bias = sc->bias;
       a.sc_cin = sc->cin;
-      sc_flops = 2.0 * n * ((h + 1) / 2) * ((wd + 1) / 2) * sc->cin * sc->cout;
+      a.sc_h = sc_h;
+      // pooled 2-D blocks: one output per pooled pixel; Conv1D: one per output row (h = rows)
+      sc_flops = sc_h > 0 ? 2.0 * n * h * sc->cin * sc->cout
+                          : 2.0 * n * ((h + 1) / 2) * ((wd + 1) / 2) * sc->cin * sc->cout;
     }
     a.pool_in = pool_in_h > 0;   // x = the unpooled [n, pool_in_h, 1, cin] (MaxPool1D fused)
     a.h_in = pool_in_h;
@@ -868,8 +872,15 @@ int run_si_net(mmla_ctx* c, const float* x, int64_t n, float* probs, int32_t* ar
                maxpool_t2_launch(X, (int)n, t, cin, XP, c->stream));
         CHK(conv_spatial(c, U.ca, XP, T1, (int)n, tp, 1, &U.bn_in, PRO_BN_RELU, EPI_BIAS, nullptr));
       }
-      CHK(conv_run(c, conv_args(U.sc, X, R, (int)n, t, 1, 2, nullptr, PRO_NONE, EPI_BIAS, nullptr)));
-      CHK(conv_spatial(c, U.cb, T1, R, (int)n, tp, 1, &U.bn_mid, PRO_BN_RELU, EPI_ADD, R));
+      if (c->precision == MMLA_PREC_F16X3 && U.cb.wh && U.sc.wh && U.sc.cout == U.cb.cout &&
+          U.sc.cout_pad == U.cb.cout_pad) {
+        // Conv1D(3) + the shortcut Conv1D(1, stride 2) of X as its residual + Add, one launch
+        CHK(conv_spatial(c, U.cb, T1, R, (int)n, tp, 1, &U.bn_mid, PRO_BN_RELU, EPI_ADD, nullptr, false,
+                         0, &U.sc, X, t));
+      } else {
+        CHK(conv_run(c, conv_args(U.sc, X, R, (int)n, t, 1, 2, nullptr, PRO_NONE, EPI_BIAS, nullptr)));
+        CHK(conv_spatial(c, U.cb, T1, R, (int)n, tp, 1, &U.bn_mid, PRO_BN_RELU, EPI_ADD, R));
+      }
       std::swap(X, R);
       t = tp;
     } else {

@@ -21,13 +21,17 @@ struct ConvH3Args {
   int pool_in;           // Conv1D only: x is [N, h_in, 1, Cin] and the conv reads MaxPool1D(2, same) of it
   int h_in;
   int* range_flag;       // nullable: set to 1 when a staged operand is >= 65504 in magnitude / inf
-  // pooled blocks (pool_out): the block's shortcut Conv2D(1x1, stride 2) of sc_x [N, H, W, sc_cin]
-  // added to the pooled output (overlap_detector_temp.py:265-270), as a 3xFP16 GEMM in the epilogue
+  // shortcut Conv(1x1, stride 2) of sc_x as a 3xFP16 GEMM in the epilogue:
+  //   pooled blocks (pool_out): sc_x [N, H, W, sc_cin], added to the pooled output
+  //     (overlap_detector_temp.py:265-270);
+  //   Conv1D (tw 1) with epi EPI_ADD: sc_x [N, sc_h, 1, sc_cin] (sc_h input rows per clip), the
+  //     residual the output adds instead of res (speaker_identification.py:179-186 pool units)
   const float* sc_x;     // nullable: no shortcut
   const uint16_t* sc_wh; // conv_h3_split_weights layout, kh = kw = 1
   const uint16_t* sc_wl;
   const float* sc_bias;  // [cout_pad]
   int sc_cin;            // multiple of 16
+  int sc_h;              // Conv1D: input rows per clip
 };
 
 // Picks the tile and launches; returns hipErrorInvalidValue for unsupported shapes.

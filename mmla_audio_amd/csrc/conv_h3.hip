@@ -83,6 +83,11 @@ constexpr int tile_px() { return BN == 64 && TW > 1 && !(KH == 3 && TW == 16) ? 
 // LIN_SLOTS, which stays zero.
 constexpr int LIN_SLOTS = 11, LIN_WP = 21;
 
+// kernel-internal epilogue: EPI_ADD whose residual is the pool unit's shortcut Conv1D(1, stride 2),
+// computed in the epilogue (ConvH3Args::sc_x); its own instantiation, with the 2-wave register
+// budget (inside the 3-wave one of the plain residual tiles it spilled)
+constexpr int EPI_ADD_SC = 3;
+
 // register estimate (accumulators + staged halo + one tap of B) up to which tap 0's B fragments are
 // loaded before the staging instead of after its barrier (above it the variants spilled)
 constexpr int EARLY_B_VGPRS = 168;
@@ -119,7 +124,8 @@ template <class S> MMLA_DEV constexpr int shp_co() { return ShapeOf<S>::co; }
 #endif
 template <int KH, int BN, int TW, int EPI, bool FIXED>
 constexpr int conv_minw() {
-  return TW == 1 && BN == 128                                       ? CONV_MINW_SI
+  return EPI == EPI_ADD_SC                                            ? 2
+         : TW == 1 && BN == 128                                       ? CONV_MINW_SI
          : (FIXED && KH == 4 && BN == 64 && TW == 8 && EPI == EPI_ADD) ? CONV_MINW_R64
                                                                      : 2;
 }
@@ -127,6 +133,8 @@ constexpr int conv_minw() {
 template <int KH, int KW, int CK, int BN, int TW, int PRO, int EPI, bool POOL, bool V4 = true,
           bool PIN = false, class SHP = Shape<0, 0, 0, 0>>
 __global__ void __launch_bounds__(NT, (conv_minw<KH, BN, TW, EPI, SHP::FIXED>())) conv_h3_kernel(ConvH3Args a) {
+  constexpr bool ADD = EPI == EPI_ADD || EPI == EPI_ADD_SC;   // the output adds a residual
+  constexpr bool SCR = EPI == EPI_ADD_SC;                     // ... the fused shortcut's
   // each wave owns ONE 32-column slice of B (no B fragment is loaded by two waves) and
   // 128 / WM rows: BN 32 -> 4 x 1, BN 64 -> 2 x 2, BN 128 -> 1 x 4 (waves along N)
   constexpr int WN = BN / 32;
@@ -154,7 +162,7 @@ __global__ void __launch_bounds__(NT, (conv_minw<KH, BN, TW, EPI, SHP::FIXED>())
   // variant (rocprof A/B): only the 8-wide residual conv(4,1) gains (blocks 5-6: 4.43 -> 4.13 ms);
   // the 3x3 and linear-pixel variants lose 2.5-6.6 % and the SI Conv1D stack 5 %.  The pooled
   // epilogue needs the pixel-row layout (its 2x2 windows inside one lane's registers).
-  constexpr bool CIL = !POOL && EPI == EPI_ADD && TW == 8;
+  constexpr bool CIL = !POOL && ADD && TW == 8;
   // Conv1D (TW == 1): one more staged row that stays zero -- a tap whose source row leaves the output
   // row's clip reads it (one select of the row offset per tap and row tile, instead of zeroing the
   // 2 x 8 halves of every A fragment read)
@@ -456,7 +464,7 @@ __global__ void __launch_bounds__(NT, (conv_minw<KH, BN, TW, EPI, SHP::FIXED>())
     const int cq = 4 * (lane >> 5);
     // the in-place residual: every load issued before the first store (see the pixel-row path)
     float4 rsd4[NTL][MT][4];
-    if constexpr (EPI == EPI_ADD) {
+    if constexpr (ADD) {
 #pragma unroll
       for (int nt = 0; nt < NTL; ++nt)
 #pragma unroll
@@ -492,7 +500,7 @@ __global__ void __launch_bounds__(NT, (conv_minw<KH, BN, TW, EPI, SHP::FIXED>())
                                  fmaf(acc[mt][nt][4 * g + 1], UNSCALE, b4[g].y),
                                  fmaf(acc[mt][nt][4 * g + 2], UNSCALE, b4[g].z),
                                  fmaf(acc[mt][nt][4 * g + 3], UNSCALE, b4[g].w));
-          if constexpr (EPI == EPI_ADD) {
+          if constexpr (ADD) {
             const float4 r = rsd4[nt][mt][g];
             v = make_float4(v.x + r.x, v.y + r.y, v.z + r.z, v.w + r.w);
           }
@@ -557,7 +565,73 @@ __global__ void __launch_bounds__(NT, (conv_minw<KH, BN, TW, EPI, SHP::FIXED>())
   // the residual is added in place (res == y): all of the lane's residual loads are issued before
   // its first store, otherwise every load waits behind the previous (possibly aliasing) store
   float rsd[NTL][MT][16];
-  if constexpr (EPI == EPI_ADD && !POOL) {
+  bool sc_res = false;
+  if constexpr (SCR && !POOL && TW == 1) {
+    // the pool unit's shortcut Conv1D(1, stride 2) computed here as the residual: a 3xFP16 GEMM whose
+    // A row is the output row's source row 2 tt of sc_x, accumulated in the main tile's layout
+    sc_res = true;
+    {
+      const size_t sks = (size_t)(A_COUTP / 32) * 512;
+      f32x16 sacc[NTL][MT];
+#pragma unroll
+      for (int nt = 0; nt < NTL; ++nt)
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) sacc[nt][mt][i] = 0.0f;
+      const float* sxp[MT];
+      bool sok[MT];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const int rg = h0 + (wm * MT + mt) * 32 + (lane & 31);   // global output row (clip, tt)
+        sok[mt] = rg < HH;
+        const int cl = (sok[mt] ? rg : 0) / A_H, tt = (sok[mt] ? rg : 0) - ((sok[mt] ? rg : 0) / A_H) * A_H;
+        sxp[mt] = a.sc_x + ((int64_t)cl * a.sc_h + 2 * tt) * a.sc_cin + koff;
+      }
+      for (int s = 0; s < a.sc_cin / 16; ++s) {
+        f16x8 bh_[NTL], bl_[NTL];
+#pragma unroll
+        for (int nt = 0; nt < NTL; ++nt) {
+          bh_[nt] = *reinterpret_cast<const f16x8*>(a.sc_wh + (size_t)s * sks + lofs[nt]);
+          bl_[nt] = *reinterpret_cast<const f16x8*>(a.sc_wl + (size_t)s * sks + lofs[nt]);
+        }
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+          float4 x0 = make_float4(0.f, 0.f, 0.f, 0.f), x1 = x0;
+          if (sok[mt]) {
+            x0 = *reinterpret_cast<const float4*>(sxp[mt] + 16 * s);
+            x1 = *reinterpret_cast<const float4*>(sxp[mt] + 16 * s + 4);
+          }
+          const float xv[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+          f16x8 xh, xl;
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            rbad |= !(fabsf(xv[k]) < ACT_RANGE);
+            const float v = xv[k] * ACT_SCALE;
+            xh[k] = (_Float16)v;
+            xl[k] = (_Float16)(v - (float)xh[k]);
+          }
+#pragma unroll
+          for (int nt = 0; nt < NTL; ++nt) {
+            sacc[nt][mt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(xh, bl_[nt], sacc[nt][mt], 0, 0, 0);
+            sacc[nt][mt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(xl, bh_[nt], sacc[nt][mt], 0, 0, 0);
+            sacc[nt][mt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(xh, bh_[nt], sacc[nt][mt], 0, 0, 0);
+          }
+        }
+      }
+#pragma unroll
+      for (int nt = 0; nt < NTL; ++nt) {
+        const int co = n0 + (wn * NTL + nt) * 32 + (lane & 31);
+        const float bsc = co < A_COUT ? a.sc_bias[co] : 0.0f;
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) rsd[nt][mt][i] = fmaf(sacc[nt][mt][i], UNSCALE, bsc);
+      }
+    }
+  }
+  if constexpr (ADD && !POOL) {
+    if (!sc_res)
 #pragma unroll
     for (int nt = 0; nt < NTL; ++nt) {
       const int co = n0 + (wn * NTL + nt) * 32 + (lane & 31);
@@ -638,7 +712,7 @@ __global__ void __launch_bounds__(NT, (conv_minw<KH, BN, TW, EPI, SHP::FIXED>())
             for (int j = 0; j < 4; ++j) {
               if (p0 + m0 + j >= npx) continue;
               float val = v[4 * g + j];
-              if constexpr (EPI == EPI_ADD) val += rsd[nt][mt][4 * g + j];
+              if constexpr (ADD) val += rsd[nt][mt][4 * g + j];
               yp[j * A_COUT] = val;
             }
             continue;
@@ -654,7 +728,7 @@ __global__ void __launch_bounds__(NT, (conv_minw<KH, BN, TW, EPI, SHP::FIXED>())
             const bool ok = TW == 1 ? (oh + j < HH) : (ow0 + j < A_W);
             if (!ok) continue;
             float val = v[4 * g + j];
-            if constexpr (EPI == EPI_ADD) val += rsd[nt][mt][4 * g + j];
+            if constexpr (ADD) val += rsd[nt][mt][4 * g + j];
             yp[j * step] = val;
           }
         }
@@ -688,7 +762,10 @@ hipError_t launch(ConvH3Args a, hipStream_t s) {
   constexpr int BMK = tile_px<KH, BN, TW>();
   // the fused pooled shortcut needs 4 m-tiles per wave (16 pooled outputs per lane) and 16-channel steps
   constexpr int WN_ = BN / 32, MT_ = BMK / ((4 / WN_) * 32);
-  if (a.sc_x && (!POOL || MT_ != 4 || a.sc_cin % 16 != 0 || a.sc_cin <= 0)) return hipErrorInvalidValue;
+  if ((EPI == EPI_ADD_SC) != (a.sc_x && !POOL)) return hipErrorInvalidValue;
+  if (a.sc_x && ((POOL ? MT_ != 4 : !(EPI == EPI_ADD_SC && TW == 1 && a.sc_h > 0)) || a.sc_cin % 16 != 0 ||
+                 a.sc_cin <= 0))
+    return hipErrorInvalidValue;
   if constexpr (TW == 0) {
     a.th = 0;
     a.tiles_w = 1;
@@ -738,6 +815,7 @@ hipError_t conv_h3_launch(ConvH3Args a, hipStream_t s) {
     a.tw = 0;
   a.tiles_w = a.tw == 0 ? 1 : (a.w + a.tw - 1) / a.tw;
   const int ck = a.cin_pad % 32 == 0 ? 32 : 16;
+  if (a.sc_x && !a.pool_out && a.epi == EPI_ADD) a.epi = EPI_ADD_SC;   // Conv1D + fused shortcut
   if (a.cin_pad % ck != 0) return hipErrorInvalidValue;
   if (a.pool_in) {   // SI pool unit: MaxPool1D(2) -> BN -> ReLU -> Conv1D(3)
     if (a.kh == 3 && a.kw == 1 && ck == 32 && a.tw == 1 && a.pro == PRO_BN_RELU &&
@@ -783,6 +861,7 @@ hipError_t conv_h3_launch(ConvH3Args a, hipStream_t s) {
   // SI-NET res_unit convs (speaker_identification.py:173-188)
   H3(3, 1, 32, 1, PRO_BN_RELU, EPI_BIAS, false)
   H3(3, 1, 32, 1, PRO_BN_RELU, EPI_ADD, false)
+  H3(3, 1, 32, 1, PRO_BN_RELU, EPI_ADD_SC, false)
 #undef H3
   return hipErrorInvalidValue;
 }
