@@ -894,10 +894,32 @@ int run_si_net(mmla_ctx* c, const float* x, int64_t n, float* probs, int32_t* ar
                                  static_cast<float*>(pseq), c->stream));
   LAUNCH(c, MMLA_STAGE_LSTM, lstm_flops(n, t / 4, 128),
          lstm_run(c, W.lstm, static_cast<float*>(pseq), n, t / 4, static_cast<float*>(ph)));
-  ConvArgs d = conv_args(W.dense, static_cast<float*>(ph), static_cast<float*>(pl), (int)n, 1, 1, 1,
-                         nullptr, PRO_NONE, EPI_BIAS, nullptr);
-  d.ldy = W.dense.cout_pad;
-  CHK(conv_run(c, d, MMLA_STAGE_HEAD));
+  if (c->precision == MMLA_PREC_F16X3 && W.dense.wh && W.dense.cin % 32 == 0) {
+    // Dense(K) as a 1x1 conv over the clips on the 3xFP16 path (conv_h3 Conv1D tiles of 128 clips):
+    // all cout_pad columns are written (the padding columns: zero weights and bias), so the logits
+    // keep the cout_pad row stride the head reads
+    ConvH3Args a{};
+    a.x = static_cast<float*>(ph);
+    a.wh = W.dense.wh;
+    a.wl = W.dense.wl;
+    a.bias = W.dense.bias;
+    a.y = static_cast<float*>(pl);
+    a.n = (int)n;
+    a.h = 1;
+    a.w = 1;
+    a.cin = a.cin_pad = W.dense.cin;
+    a.cout = a.cout_pad = W.dense.cout_pad;
+    a.kh = a.kw = 1;
+    a.pro = PRO_NONE;
+    a.epi = EPI_BIAS;
+    a.range_flag = c->range_ptr;
+    LAUNCH(c, MMLA_STAGE_HEAD, 2.0 * n * W.dense.cin * W.dense.cout, conv_h3_launch(a, c->stream));
+  } else {
+    ConvArgs d = conv_args(W.dense, static_cast<float*>(ph), static_cast<float*>(pl), (int)n, 1, 1, 1,
+                           nullptr, PRO_NONE, EPI_BIAS, nullptr);
+    d.ldy = W.dense.cout_pad;
+    CHK(conv_run(c, d, MMLA_STAGE_HEAD));
+  }
   LAUNCH(c, MMLA_STAGE_HEAD, 4.0 * n * W.k,
          si_head_launch(static_cast<float*>(pl), (int)n, W.k, W.dense.cout_pad, W.head, probs,
                         argmax, silent, c->stream));
