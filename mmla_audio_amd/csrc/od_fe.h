@@ -22,10 +22,12 @@ struct OdFeTables {
   //   stage 2, gemm k2' = 0..12: rows 2 i + ri,    k = 2 n1 + ri (twiddle x DFT-16, x 2^8)
   uint16_t a1[16][2][2][64][8];
   uint16_t a2[13][2][2][64][8];
-  // v3 mel: band pairs (2 ib, 2 ib + 1) scheduled over the waves of a workgroup with balanced taps:
-  // mel_pair[nw][w * (64 / nw) + k] = k-th pair of wave w when the workgroup has nw waves (4..16)
-  int mel_pair[17][64];
-  int mel_pair_taps[64];    // max non-zeros of the pair's two bands
+  // v3 mel on the f32 MFMA (v_mfma_f32_16x16x4f32): 8 tiles of 16 bands x the two 16-frame halves of
+  // a 32-frame tile = 16 units, one per wave.  Band tile bt reads P rows mel_bt_bin0[bt] .. + 4 nk - 1
+  // (nk = mel_bt_nk[bt], a multiple of 4) against A fragments mel_bt_frag[bt] .. + nk - 1
+  int mel_bt_bin0[8], mel_bt_nk[8], mel_bt_frag[8];
+  int mel_unit[16];         // wave -> 2 bt + frame half; per SIMD (waves w, w + 4, w + 8, w + 12) balanced
+  float mel_a[64][64];      // A fragments [frag][lane]: A[m = l & 15][k = l >> 4] = mel_w[16 bt + m][bin0 + 4 j + k] x 2^-38
   uint16_t zero16;          // a zero sample: the target of reads past a clip's length
 };
 

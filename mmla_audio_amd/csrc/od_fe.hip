@@ -39,6 +39,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <cstring>
 #include <type_traits>
 #include <utility>
 
@@ -686,10 +687,9 @@ constexpr int ZP = 36;                        // Z row pitch (halves): 18 dwords
 constexpr int PP = 34;                        // P row pitch (floats)
 constexpr int PROWS = 212;                    // bins 0..200 + zero rows read by the last mel taps
 constexpr int PTRASH = PROWS;                 // + one row that stage 2's unused lanes write
-constexpr int MW = 12;                        // mel taps stored per band (zero-padded: 4-tap batches)
 constexpr int G1 = 16 / NWV;                  // stage-1 GEMMs (n1) per wave
 constexpr int G2 = (13 + NWV - 1) / NWV;      // stage-2 GEMMs (k2') per wave (the last round partial)
-constexpr int PPW = 64 / NWV;                 // mel band pairs per wave
+constexpr int MFRAG = 64;                     // mel A fragments (16 bands x 4 bins each)
 constexpr int ROT4 = 9;                       // tile 4: chunk c is staged by thread c + ROT4
 static_assert(NCH + ROT4 <= NTH, "one staged chunk per thread");
 static_assert(G1 == 1, "stage 1: one GEMM per wave (16 waves)");
@@ -701,9 +701,8 @@ static_assert(16 % NWV == 0 && 64 % NWV == 0, "work split over the waves");
 struct Smem {
   // the buffers read at lane-dependent addresses plus constant offsets first: their offsets stay
   // below 64 KB, the ds instructions' immediate field (else a VALU add per read)
-  float p[(PROWS + 1) * PP + 64];             // power [bin][frame] (+ the trash row)
-  alignas(16) float mw[128 * MW];             // mel taps [band][j] x P_SCALE (zero past the band's non-zeros)
-  int mst[128];                               // first bin of each band x PP (its P row offset)
+  float p[2][(PROWS + 1) * PP + 64];          // power [bin][frame] (+ the trash row), by step parity
+  float ma[MFRAG * 64];                       // mel A fragments (OdFeTables::mel_a), x P_SCALE
   uint32_t ztrash[128];                       // stage 1's one unused (k2 = 14) word per lane, hi / lo
   uint32_t t[16 * TP];                        // staged samples, transposed: (hi, lo) fp16 pair of x'[16 q + n1]
   _Float16 z_hi[13 * TF * ZP], z_lo[13 * TF * ZP];   // stage-1 output
@@ -734,6 +733,16 @@ MMLA_DEV void split2(float a, float b, uint32_t& hi, uint32_t& lo) {
   asm("v_fma_mixlo_f16 %0, %1, 1.0, -%2 op_sel_hi:[0,0,1]\n\t"
       "v_fma_mixhi_f16 %0, %3, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
       : "=&v"(lo) : "v"(a), "v"(hi), "v"(b));
+}
+
+// raw buffer descriptor over [p, p + bytes): p must be wave-uniform (its halves are readfirstlane'd
+// so the descriptor lives in SGPRs); a null p gives zero records (every access dropped)
+MMLA_DEV __amdgpu_buffer_rsrc_t wave_rsrc(const void* p, uint32_t bytes) {
+  const uint64_t u = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)u);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(u >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), (short)0,
+                                           (int)bytes, 0x00020000);
 }
 
 MMLA_DEV uint32_t pack_f16(_Float16 a, _Float16 b) {
@@ -837,9 +846,8 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
       a2l[j][s] = *reinterpret_cast<const f16x8*>(tb.a2[k2][s][1][lane]);
     }
   }
-  for (int i = tid; i < 128 * MW; i += NTH) sm.mw[i] = i % MW < 10 ? tb.mel_w[i / MW][i % MW] * P_SCALE : 0.0f;
-  for (int i = tid; i < 128; i += NTH) sm.mst[i] = tb.mel_start[i] * PP;
-  for (int i = tid; i < (PROWS - 201) * PP; i += NTH) sm.p[201 * PP + i] = 0.0f;
+  for (int i = tid; i < MFRAG * 64; i += NTH) sm.ma[i] = (&tb.mel_a[0][0])[i];
+  for (int i = tid; i < 2 * (PROWS - 201) * PP; i += NTH) sm.p[i & 1][201 * PP + (i >> 1)] = 0.0f;
   for (int i = tid; i < 16 * (TP - TQS); i += NTH) sm.t[(i / (TP - TQS)) * TP + TQS + i % (TP - TQS)] = 0u;
   if (tid == 0) sm.sgn[0] = 0;
 
@@ -882,15 +890,18 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
     if (clip_ >= n_clips) return;
     const ClipIn ci = clip_in(clip_);
     if (!ci.fast) return;
+    // a buffer load over the clip's readable samples: chunks before sample 0 (negative offsets wrap
+    // past the range) and past len read zeros with no per-lane bounds arithmetic; threads without a
+    // chunk (c >= NCH) load harmlessly and never store
+    const auto rs = wave_rsrc(ci.src, (uint32_t)ci.len * 2u);
     const int c = stid() - (t == NTILE - 1 ? ROT4 : 0);
-    const int i0 = HOP * TF * t - N_FFT / 2 + 8 * c;
-    if (c >= 0 && c < NCH && i0 >= 0 && i0 + 8 <= ci.len) {
-      const uint4 v = *reinterpret_cast<const uint4*>(ci.src + i0);
-      nx[0] = v.x;
-      nx[1] = v.y;
-      nx[2] = v.z;
-      nx[3] = v.w;
-    }
+    const uint32_t off = (uint32_t)(2 * (HOP * TF * t - N_FFT / 2 + 8 * c));
+    typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+    const u4v v = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+    nx[0] = v.x;
+    nx[1] = v.y;
+    nx[2] = v.z;
+    nx[3] = v.w;
   };
 
   // ---- staging of (clip, t): chunk c holds p = 8c .. 8c + 7 (reflect-padded, zero past len), split
@@ -1071,7 +1082,7 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
 
   // ---- stage 2 (wave = k2' wid + NWV j): D2 = A2[k2'] (32 x 32) . Z[k2'] (32 k x 32 frames)
   //      -> |X|^2 (x 2^38: P_SCALE sits in the mel weights) -> P[bin][frame] ------------------------
-  auto stage2 = [&](int r, int hh) {
+  auto stage2 = [&](int r, int hh, float* P) {
 #pragma unroll
     for (int j = 0; j < G2; ++j) {
       const int k2 = wid + NWV * j;
@@ -1092,8 +1103,8 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
       // pair i = c0 + 2 hh (c0 = (pi & 1) + 4 (pi >> 1)): bin 25 i + k2 (i < 8: c0 < 8), else
       // 25 (i - 8) + 25 - k2; GEMM 0 has bins 25 i for i <= 8 only (the other lanes write the
       // trash row).  Branch-free: the row offset is an immediate plus the wave-uniform k2
-      float* prow = sm.p + 50 * PP * hh + r;
-      float* trash = sm.p + PTRASH * PP + lane;
+      float* prow = P + 50 * PP * hh + r;
+      float* trash = P + PTRASH * PP + lane;
 #pragma unroll
       for (int pi = 0; pi < 8; ++pi) {
         const int c0 = (pi & 1) + 4 * (pi >> 1);
@@ -1128,49 +1139,49 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
     }
   };
 
-  // mel band pairs of this wave (2 ib + hh is this lane's band) and their wave-uniform tap counts
-  int pair[PPW], ptaps[PPW];
-#pragma unroll
-  for (int k = 0; k < PPW; ++k) {
-    pair[k] = __builtin_amdgcn_readfirstlane(tb.mel_pair[NWV][wid * PPW + k]);
-    ptaps[k] = __builtin_amdgcn_readfirstlane(tb.mel_pair_taps[pair[k]]);
-  }
-  // 10 log10 S of this lane's band of each pair at frame 32 t + r
-  float dbv[NTILE][PPW];
+  // this wave's mel unit: band tile bt (bands 16 bt ..), frame half fh of the 32-frame tile
+  const int m_unit = __builtin_amdgcn_readfirstlane(tb.mel_unit[wid]);
+  const int m_bt = m_unit >> 1, m_fh = m_unit & 1;
+  const int m_bin0 = __builtin_amdgcn_readfirstlane(tb.mel_bt_bin0[m_bt]);
+  const int m_nk = __builtin_amdgcn_readfirstlane(tb.mel_bt_nk[m_bt]);
+  const int m_frag = __builtin_amdgcn_readfirstlane(tb.mel_bt_frag[m_bt]);
+  // 10 log10 S at band 16 bt + 4 (l >> 4) + i, frame 32 t + 16 fh + (l & 15)
+  float dbv[NTILE][4];
   float smax = 0.0f, smin = INFINITY;
+  typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-  // ---- mel of tile t (lane = frame r x band 2 ib + hh of each of the wave's pairs ib; the pair's tap
-  //      count is wave-uniform, taps past a band's own count are zero weights) -> 10 log10 S --------
-  auto mel = [&](auto T_, int r, int hh) {
+  // ---- mel of tile t on the f32 MFMA: S[16 bands][16 frames] = A (16 x 4 k-steps) . P (bins x frames),
+  //      exact float32 products and sums (the reference's np.dot is float32); K-steps in batches of 4
+  //      whose 8 LDS reads are issued before their MFMAs; A columns past a band's support are zero ----
+  auto mel = [&](auto T_, const float* P) {
     constexpr int t = decltype(T_)::value;
+    int l = lane;
+    asm volatile("" : "+v"(l));
+    const float* pb = P + (m_bin0 + (l >> 4)) * PP + 16 * m_fh + (l & 15);
+    const float* ab = sm.ma + m_frag * 64 + l;
+    f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+    int nk = m_nk;
+    asm volatile("" : "+s"(nk));
+    constexpr int NK_MAX = 20;
 #pragma unroll
-    for (int k = 0; k < PPW; ++k) {
-      if (FE3_SKIP & 8) break;
-      const int b = 2 * pair[k] + hh;
-      const float* wp = sm.mw + b * MW;
-      const float* pp = sm.p + sm.mst[b] + r;
-      float sacc = 0.0f;
-      // taps in batches of 4 (the batch's reads issued before its FMAs): zero weights past the
-      // band's own taps, P rows past bin 200 are zero.  (Batches of 1, 1, 2, 4, 4 read 33 % fewer
-      // taps but cost more LDS round trips: the interval got 9 % longer.)  The tap count is made
-      // opaque per use: the compiler otherwise precomputes all batch conditions of all tiles as SGPR
-      // masks, which spill into VGPR lanes
-      int nt = ptaps[k];
-      asm volatile("" : "+s"(nt));
+    for (int j0 = 0; j0 < NK_MAX; j0 += 4) {
+      if ((FE3_SKIP & 8) || j0 >= nk) break;
+      float av[4], bv[4];
 #pragma unroll
-      for (int j0 = 0; j0 < MW; j0 += 4) {
-        if (j0 >= nt) break;
-        const float4 w4 = *reinterpret_cast<const float4*>(wp + j0);
-        const float p0 = pp[j0 * PP], p1 = pp[(j0 + 1) * PP], p2 = pp[(j0 + 2) * PP], p3 = pp[(j0 + 3) * PP];
-        sacc = fmaf(w4.x, p0, sacc);
-        sacc = fmaf(w4.y, p1, sacc);
-        sacc = fmaf(w4.z, p2, sacc);
-        sacc = fmaf(w4.w, p3, sacc);
+      for (int j = 0; j < 4; ++j) {
+        av[j] = ab[64 * (j0 + j)];
+        bv[j] = pb[4 * PP * (j0 + j)];
       }
-      dbv[t][k] = db10m(sacc);
-      if (TF * t + TF <= NF || TF * t + r < NF) {
-        smax = fmaxf(smax, sacc);
-        smin = fminf(smin, sacc);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j], bv[j], acc, 0, 0, 0);
+    }
+    const bool live = TF * t + TF <= NF || TF * t + 16 * m_fh + (l & 15) < NF;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      dbv[t][i] = db10m(acc[i]);
+      if (live) {
+        smax = fmaxf(smax, acc[i]);
+        smin = fminf(smin, acc[i]);
       }
     }
   };
@@ -1178,7 +1189,7 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
   // ---- a clip's end: max / min of its mel power over the waves, power_to_db(ref=np.max, amin=1e-10,
   //      top_db=80) with numpy-1.21 dtypes, normalize_matrix (max / min of the dB matrix are the dB
   //      of max / min S, as v2), stores straight from the registers -----------------------------------
-  auto epilogue = [&](int64_t clip, int par, int r, int hh) {
+  auto epilogue = [&](int64_t clip, int par) {
 #pragma clang fp contract(off)
     float mx = sm.red[0][0], mn = sm.red[1][0];
 #pragma unroll
@@ -1197,32 +1208,44 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
     const float inv_diff = 1.0f / diff;
     const int tz = otid();
     if (a.zcr && tz < NF) a.zcr[clip * NF + tz] = (float)sm.zc[par][tz] * (1.0f / 400.0f);
-    // norm / dB rows: lane (r, hh) of a pair writes frame 32 t + r of band 2 ib + hh -- 128 B of
-    // one band row per half-wave.  Image (rows h = 127 - band, RGB bytes): R = trunc(255 zcr[w]),
-    // G = B = trunc(255 (1 - norm)) in float64, NaN -> 0; three byte stores per pixel
-    const int64_t ob = clip * (int64_t)(NMEL * NF) + r;
+    // norm / dB rows: lane l writes frame 32 t + 16 fh + (l & 15) of bands 16 bt + 4 (l >> 4) + i --
+    // 64 B of one band row per 16 lanes.  Image (rows h = 127 - band, RGB bytes): R = trunc(255 zcr[w]),
+    // G = B = trunc(255 (1 - norm)) in float64, NaN -> 0; three byte stores per pixel.
+    // Buffer stores over the clip's output block: the lane's offset is one VGPR, the unit's band tile /
+    // frame half an SGPR and (i, t) the immediate -- no per-store address arithmetic
+    constexpr uint32_t FB = NMEL * NF * 4, IB = NMEL * NF * 3;
+    const auto rn = wave_rsrc(NM ? a.norm + clip * (NMEL * NF) : nullptr, NM ? FB : 0);
+    const auto rd = wave_rsrc(DB ? a.db + clip * (NMEL * NF) : nullptr, DB ? FB : 0);
+    const auto ri = wave_rsrc(IMG ? a.img + clip * (NMEL * NF * 3) : nullptr, IMG ? IB : 0);
+    int l = lane;
+    asm volatile("" : "+v"(l));
+    const int fr = 16 * m_fh + (l & 15);                          // frame within the 32-frame tile
+    const uint32_t vf = (uint32_t)(4 * (l >> 4) * NF + (l & 15)) * 4u;
+    const int sf = (16 * m_bt * NF + 16 * m_fh) * 4;
+    // image row 127 - (16 bt + 4 (l >> 4) + i) = (112 - 16 bt) + (12 - 4 (l >> 4)) + (3 - i)
+    const uint32_t vi = (uint32_t)((12 - 4 * (l >> 4)) * NF + (l & 15)) * 3u;
+    const int si = ((112 - 16 * m_bt) * NF + 16 * m_fh) * 3;
 #pragma unroll
-    for (int k = 0; k < PPW; ++k) {
-      const int b = 2 * pair[k] + hh;
-      float* qn = NM ? a.norm + ob + b * NF : nullptr;
-      float* qd = DB ? a.db + ob + b * NF : nullptr;
-      uint8_t* qi = IMG ? a.img + clip * (int64_t)(NMEL * NF * 3) + ((NMEL - 1 - b) * NF + r) * 3 : nullptr;
+    for (int t = 0; t < NTILE; ++t) {
+      if (TF * t + TF > NF && TF * t + fr >= NF) continue;
+      uint32_t rr = 0;
+      if (IMG) rr = (uint32_t)(int)(((double)sm.zc[par][TF * t + fr] / 400.0) * 255.0) & 255u;
 #pragma unroll
-      for (int t = 0; t < NTILE; ++t) {
-        if (TF * t + TF > NF && TF * t + r >= NF) continue;
-        const float d = fmaxf(dbv[t][k] - ref_db, thr);
+      for (int i = 0; i < 4; ++i) {
+        const float d = fmaxf(dbv[t][i] - ref_db, thr);
         // (d - min) / (max - min) as a multiply by the reciprocal (<= 2 ulp; as v2); 0 * inf =
         // NaN keeps the digital-silence NaN
         const float nv = (d - d_min) * inv_diff;
-        if (NM && !(FE3_SKIP & 16)) qn[TF * t] = nv;
-        if (DB) qd[TF * t] = d;
+        const uint32_t of = vf + (uint32_t)(i * NF + TF * t) * 4u;
+        if (NM && !(FE3_SKIP & 16)) __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, nv), rn, of, sf, 0);
+        if (DB) __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, d), rd, of, sf, 0);
         if (IMG) {
           const double v = (1.0 - (double)nv) * 255.0;
-          const uint8_t gb = (v >= 0.0) ? (uint8_t)((uint32_t)(int)v & 255u) : (uint8_t)0;
-          const uint8_t rr = (uint8_t)(int)(((double)sm.zc[par][TF * t + r] / 400.0) * 255.0);
-          qi[3 * TF * t] = rr;
-          qi[3 * TF * t + 1] = gb;
-          qi[3 * TF * t + 2] = gb;
+          const uint32_t gb = (v >= 0.0) ? ((uint32_t)(int)v & 255u) : 0u;
+          const uint32_t oi = vi + (uint32_t)((3 - i) * NF + TF * t) * 3u;
+          __builtin_amdgcn_raw_buffer_store_b8((uint8_t)rr, ri, oi, si, 0);
+          __builtin_amdgcn_raw_buffer_store_b8((uint8_t)gb, ri, oi + 1, si, 0);
+          __builtin_amdgcn_raw_buffer_store_b8((uint8_t)gb, ri, oi + 2, si, 0);
         }
       }
     }
@@ -1251,21 +1274,38 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
     const int par = (int)(ci & 1);
     for_tiles([&](auto T_) {
       constexpr int t = decltype(T_)::value;
-      if (!cur && t > 0) return;
+      // the drain pass after the last clip: step 0's interval B (mel of the last tile, max / min) and
+      // step 1's interval A (the last clip's epilogue)
+      if (!cur && t > 1) return;
       // lane-derived offsets are recomputed per tile from an opaque copy of the lane id: hoisted,
       // the per-band store / LDS addresses of all five tiles stay live together and spill
       int lane_o = lane;
       asm volatile("" : "+v"(lane_o));
       const int r = lane_o & 31, hh = lane_o >> 5;
+      // P by step parity: stage 2 of step s writes P[s & 1] while the mel of step s - 1 reads the other
+      const int pw = (int)((ci * NTILE + t) & 1);
+      float* const p_w = sm.p[pw];
+      const float* const p_r = sm.p[pw ^ 1];
       // ---- interval A ----
       if (cur) {
         crossings(T_);
         stage1(r, hh);
       }
+      if (t == 1 && ci > 0) {   // the previous clip: its last mel and max / min finished in step 0
+        epilogue(clip - gridDim.x, par ^ 1);
+        FE3_MARK(4);
+        FE3_T_STORE(clip - gridDim.x);
+      }
+      FE3_MARK(0);
+      __syncthreads();
+      FE3_MARK(1);
+      if (!cur && t == 1) return;
+      // ---- interval B ----
+      if (cur) stage2(r, hh, p_w);
       if constexpr (t > 0) {
-        mel(tile_c<t - 1>{}, r, hh);
+        mel(tile_c<t - 1>{}, p_r);
       } else if (ci > 0) {
-        mel(tile_c<NTILE - 1>{}, r, hh);
+        mel(tile_c<NTILE - 1>{}, p_r);
         const float mx = wave_red<true>(smax), mn = wave_red<false>(smin);
         if (lane == 0) {
           sm.red[0][wid] = mx;
@@ -1274,12 +1314,7 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
         smax = 0.0f;
         smin = INFINITY;
       }
-      FE3_MARK(0);
-      __syncthreads();
-      FE3_MARK(1);
-      // ---- interval B ----
       if (cur) {
-        stage2(r, hh);
         zsum(T_, par);
         if constexpr (t + 1 < NTILE) {
           stage(clip, tile_c<t + 1>{});
@@ -1293,12 +1328,7 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
         }
       }
       FE3_MARK(2);
-      if (t == 0 && ci > 0) {
-        epilogue(clip - gridDim.x, par ^ 1, r, hh);
-        FE3_MARK(4);
-        FE3_T_STORE(clip - gridDim.x);
-      }
-      if (cur) __syncthreads();
+      __syncthreads();
       FE3_MARK(3);
     }, std::make_integer_sequence<int, NTILE>{});
   }
@@ -1321,9 +1351,19 @@ bool od_fe_tables_ok(const OdFeTables& t) {
   if (t.mel_taps_lo > v2::T_LO || t.mel_taps_hi > v2::T_HI) return false;
   for (int m = 0; m < 128; ++m) {  // the last tap of every band stays inside the zero-padded row
     if (t.mel_start[m] + (m < 64 ? v2::T_LO : v2::T_HI) > v2::P2W) return false;
-    const int batched = (t.mel_pair_taps[m / 2] + 3) / 4 * 4;   // v3 reads 4-tap batches
-    if (batched > v3::MW || t.mel_start[m] + batched > v3::PROWS) return false;
+    const int bt = m / 16;   // v3: the band's support lies inside its tile's bins, read rows stay in P
+    if (t.mel_cnt[m] > 0 && (t.mel_start[m] < t.mel_bt_bin0[bt] ||
+                             t.mel_start[m] + t.mel_cnt[m] > t.mel_bt_bin0[bt] + 4 * t.mel_bt_nk[bt]))
+      return false;
   }
+  int frags = 0;
+  for (int bt = 0; bt < 8; ++bt) {
+    if (t.mel_bt_nk[bt] % 4 || t.mel_bt_nk[bt] > 20 || t.mel_bt_bin0[bt] < 0 ||
+        t.mel_bt_bin0[bt] + 4 * t.mel_bt_nk[bt] > v3::PROWS || t.mel_bt_frag[bt] != frags)
+      return false;
+    frags += t.mel_bt_nk[bt];
+  }
+  if (frags > v3::MFRAG) return false;
   return true;
 }
 
@@ -1470,23 +1510,44 @@ void od_fe_build_tables(OdFeTables* t) {
     taps = cnt > taps ? cnt : taps;
   }
 
-  // v3 mel schedule: pairs of adjacent bands (one per half-wave), longest first onto the wave with
-  // the fewest taps so far (every wave gets 64 / nw pairs)
-  for (int ib = 0; ib < 64; ++ib)
-    t->mel_pair_taps[ib] = std::max(t->mel_cnt[2 * ib], t->mel_cnt[2 * ib + 1]);
-  for (int nw = 0; nw <= 16; ++nw) {
-    for (int k = 0; k < 64; ++k) t->mel_pair[nw][k] = k;
-    if (nw < 1 || 64 % nw) continue;
-    int order[64];
-    for (int k = 0; k < 64; ++k) order[k] = k;
-    std::stable_sort(order, order + 64, [&](int x, int y) { return t->mel_pair_taps[x] > t->mel_pair_taps[y]; });
-    int load[16] = {0}, fill[16] = {0};
-    for (int k = 0; k < 64; ++k) {
+  // v3 mel schedule: band tile bt = bands 16 bt .. 16 bt + 15 reads the bins of their union, in
+  // k-steps of 4 bins, padded to batches of 4 k-steps and kept inside the P rows (start moved down)
+  std::memset(t->mel_a, 0, sizeof(t->mel_a));
+  int frag = 0;
+  for (int bt = 0; bt < 8; ++bt) {
+    int lo = 1 << 30, hi = -1;
+    for (int m = 16 * bt; m < 16 * bt + 16; ++m)
+      if (t->mel_cnt[m] > 0) {
+        lo = std::min(lo, t->mel_start[m]);
+        hi = std::max(hi, t->mel_start[m] + t->mel_cnt[m] - 1);
+      }
+    if (hi < 0) lo = hi = 0;
+    const int nk = ((hi - lo + 1 + 3) / 4 + 3) / 4 * 4;
+    const int b0 = std::max(0, std::min(lo, v3::PROWS - 4 * nk));
+    t->mel_bt_bin0[bt] = b0;
+    t->mel_bt_nk[bt] = nk;
+    t->mel_bt_frag[bt] = frag;
+    for (int j = 0; j < nk && frag + j < v3::MFRAG; ++j)
+      for (int l = 0; l < 64; ++l) {
+        const int m = 16 * bt + (l & 15), bin = b0 + 4 * j + (l >> 4);
+        const int jj = bin - t->mel_start[m];
+        if (jj >= 0 && jj < t->mel_cnt[m] && jj < 10) t->mel_a[frag + j][l] = t->mel_w[m][jj] * v3::P_SCALE;
+      }
+    frag += nk;
+  }
+  // units (bt, frame half) onto waves: longest first onto the SIMD with the least MFMA work so far,
+  // four units per SIMD (a SIMD runs waves s, s + 4, s + 8, s + 12)
+  {
+    int order[16];
+    for (int u = 0; u < 16; ++u) order[u] = u;
+    std::stable_sort(order, order + 16, [&](int x, int y) { return t->mel_bt_nk[x >> 1] > t->mel_bt_nk[y >> 1]; });
+    int load[4] = {0, 0, 0, 0}, fill[4] = {0, 0, 0, 0};
+    for (int k = 0; k < 16; ++k) {
       int best = -1;
-      for (int w = 0; w < nw; ++w)
-        if (fill[w] < 64 / nw && (best < 0 || load[w] < load[best])) best = w;
-      t->mel_pair[nw][best * (64 / nw) + fill[best]++] = order[k];
-      load[best] += t->mel_pair_taps[order[k]];
+      for (int s_ = 0; s_ < 4; ++s_)
+        if (fill[s_] < 4 && (best < 0 || load[s_] < load[best])) best = s_;
+      t->mel_unit[best + 4 * fill[best]++] = order[k];
+      load[best] += t->mel_bt_nk[order[k] >> 1];
     }
   }
 
