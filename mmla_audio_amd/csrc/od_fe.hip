@@ -1300,8 +1300,8 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
       __syncthreads();
       FE3_MARK(1);
       if (!cur && t == 1) return;
-      // ---- interval B ----
-      if (cur) stage2(r, hh, p_w);
+      // ---- interval B ----  (the mel of tile t - 1 first: its MFMAs then start on every wave at the
+      // barrier instead of queueing behind stage 2's on waves 0-12 -- 0.2975 -> 0.2903 ms, A/B)
       if constexpr (t > 0) {
         mel(tile_c<t - 1>{}, p_r);
       } else if (ci > 0) {
@@ -1314,6 +1314,7 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
         smax = 0.0f;
         smin = INFINITY;
       }
+      if (cur) stage2(r, hh, p_w);
       if (cur) {
         zsum(T_, par);
         if constexpr (t + 1 < NTILE) {
