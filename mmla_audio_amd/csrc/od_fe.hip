@@ -690,6 +690,10 @@ constexpr int PTRASH = PROWS;                 // + one row that stage 2's unused
 constexpr int G1 = 16 / NWV;                  // stage-1 GEMMs (n1) per wave
 constexpr int G2 = (13 + NWV - 1) / NWV;      // stage-2 GEMMs (k2') per wave (the last round partial)
 constexpr int MFRAG = 64;                     // mel A fragments (16 bands x 4 bins each)
+#ifndef FE3_MEL_A_W0
+#define FE3_MEL_A_W0 16   // measured: 12 (the youngest wave of each SIMD in A) 0.2964 ms, 8: 0.2944, 14: 0.3054, 16: 0.2941
+#endif
+constexpr int MEL_A_W0 = FE3_MEL_A_W0;         // waves >= this run the mel in interval A (16: none)
 constexpr int ROT4 = 9;                       // tile 4: chunk c is staged by thread c + ROT4
 static_assert(NCH + ROT4 <= NTH, "one staged chunk per thread");
 static_assert(G1 == 1, "stage 1: one GEMM per wave (16 waves)");
@@ -1286,6 +1290,16 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
       const int pw = (int)((ci * NTILE + t) & 1);
       float* const p_w = sm.p[pw];
       const float* const p_r = sm.p[pw ^ 1];
+      // the mel of the previous step reads P[(s - 1) & 1], stable through intervals A and B of step s:
+      // waves >= MEL_A_W0 (the youngest of each SIMD, last to finish the heavier interval B) run it in A
+      auto mel_prev = [&]() {
+        if constexpr (t > 0) {
+          mel(tile_c<t - 1>{}, p_r);
+        } else if (ci > 0) {
+          mel(tile_c<NTILE - 1>{}, p_r);
+        }
+      };
+      const bool mel_a = wid >= MEL_A_W0;
       // ---- interval A ----
       if (cur) {
         crossings(T_);
@@ -1296,16 +1310,15 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
         FE3_MARK(4);
         FE3_T_STORE(clip - gridDim.x);
       }
+      if (mel_a) mel_prev();   // (after the epilogue: tile 0's mel overwrites the dB registers it read)
       FE3_MARK(0);
       __syncthreads();
       FE3_MARK(1);
       if (!cur && t == 1) return;
       // ---- interval B ----  (the mel of tile t - 1 first: its MFMAs then start on every wave at the
       // barrier instead of queueing behind stage 2's on waves 0-12 -- 0.2975 -> 0.2903 ms, A/B)
-      if constexpr (t > 0) {
-        mel(tile_c<t - 1>{}, p_r);
-      } else if (ci > 0) {
-        mel(tile_c<NTILE - 1>{}, p_r);
+      if (!mel_a) mel_prev();
+      if (t == 0 && ci > 0) {
         const float mx = wave_red<true>(smax), mn = wave_red<false>(smin);
         if (lane == 0) {
           sm.red[0][wid] = mx;
