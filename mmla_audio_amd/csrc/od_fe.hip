@@ -864,7 +864,11 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
   };
   // the staging thread order starts at wave SW0: waves 13..15 (no stage-2 GEMM) take the first 192
   // chunks, so interval B's staging lands mostly on the waves stage 2 leaves idle
-  constexpr int SW0 = 13;
+#ifndef FE3_SW0
+#define FE3_SW0 0   // 13 (waves 13-15 first) was best with the mel in interval A; with it in B, 0:
+                    //   0.2899 vs 0.2936 ms (8: 0.2951), A/B 3 rounds
+#endif
+  constexpr int SW0 = FE3_SW0;
   auto stid = [&]() { return (otid() + (NWV - SW0) * 64) & (NTH - 1); };
   static_assert(NWV == 16, "staging order assumes 16 waves");
 
