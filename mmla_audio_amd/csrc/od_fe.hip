@@ -862,8 +862,8 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
     asm volatile("" : "+v"(v));
     return v;
   };
-  // the staging thread order starts at wave SW0: waves 13..15 (no stage-2 GEMM) take the first 192
-  // chunks, so interval B's staging lands mostly on the waves stage 2 leaves idle
+  // the staging thread order starts at wave SW0 (chunk c is staged by thread c + 64 (16 - SW0), mod
+  // 1024): which waves carry interval B's staging beside the mel and stage 2
 #ifndef FE3_SW0
 #define FE3_SW0 0   // 13 (waves 13-15 first) was best with the mel in interval A; with it in B, 0:
                     //   0.2899 vs 0.2936 ms (8: 0.2951), A/B 3 rounds
