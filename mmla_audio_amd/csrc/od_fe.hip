@@ -1554,12 +1554,19 @@ void od_fe_build_tables(OdFeTables* t) {
     frag += nk;
   }
   // units (bt, frame half) onto waves: longest first onto the SIMD with the least MFMA work so far,
-  // four units per SIMD (a SIMD runs waves s, s + 4, s + 8, s + 12)
+  // four units per SIMD (a SIMD runs waves s, s + 4, s + 8, s + 12).  The mel shares interval B with
+  // stage 2, whose 13 GEMMs (6 MFMAs of the mel K-step's 32 cycles each) sit on waves 0-12: SIMD 0
+  // starts with 4 of them, the others with 3 (FE3_MEL_S2LOAD 0: mel work alone)
+#ifndef FE3_MEL_S2LOAD
+#define FE3_MEL_S2LOAD 1
+#endif
   {
     int order[16];
     for (int u = 0; u < 16; ++u) order[u] = u;
     std::stable_sort(order, order + 16, [&](int x, int y) { return t->mel_bt_nk[x >> 1] > t->mel_bt_nk[y >> 1]; });
     int load[4] = {0, 0, 0, 0}, fill[4] = {0, 0, 0, 0};
+    if (FE3_MEL_S2LOAD)
+      for (int w = 0; w < 13; ++w) load[w % 4] += 6;
     for (int k = 0; k < 16; ++k) {
       int best = -1;
       for (int s_ = 0; s_ < 4; ++s_)
