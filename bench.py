@@ -169,28 +169,60 @@ def sample_indices(n, mb, k, seed=20261015):
     return sorted(idx)
 
 
-def parity_sample(ctx, wl, pcm, probs, argmax, W, mb, clip_len, k=24):
+def fe_sample_indices(n, grid, k=24, seed=20261015):
+    """od_features: clips the persistent front-end's workgroups run first, in the middle and last
+    (workgroup b owns clips b, b + grid, ...) + k seeded random clips"""
+    idx = {0, n - 1}
+    for b in (0, grid // 3, grid // 2, grid - 1):
+        owned = list(range(b, n, grid))
+        if owned:
+            idx.update((owned[0], owned[len(owned) // 2], owned[-1]))
+    idx.update(np.random.default_rng(seed).choice(n, min(k, n), replace=False).tolist())
+    return sorted(i for i in idx if 0 <= i < n)
+
+
+def parity_sample(ctx, wl, pcm, probs, argmax, W, mb, clip_len, k=24, fe_out=None):
     """oracle (float64) vs the timed run's outputs on clips spread across the whole batch"""
     from oracle import od_fe, si_fe
     from oracle.nets_torch import Nets
     n = pcm.shape[0]
-    idx = sample_indices(n, mb, k)
+    if wl == 'od_features':
+        grid = min(n, torch.cuda.get_device_properties(pcm.device).multi_processor_count)
+        idx = fe_sample_indices(n, grid, k)
+    else:
+        idx = sample_indices(n, mb, k)
     sub = pcm[idx].contiguous()
     host = sub.cpu().numpy()
     out = {'sample_clips': len(idx), 'sample': 'first + last clip of every micro-batch and '
            f'{min(k, n)} seeded random clips of the {n}-clip batch; float64 oracle'}
-    if wl in ('od_pipeline', 'od_features'):
-        norm = torch.empty((len(idx), 128, 151), dtype=torch.float32, device='cuda')
-        ctx.od_features_dev(sub.data_ptr(), len(idx), clip_len, clip_len, norm=norm.data_ptr())
+    if wl == 'od_features':
+        # the TIMED run's own outputs (the last timed step wrote norm / zcr), at clips that the
+        # persistent workgroups process first, in the middle and last
+        out['sample'] = (f'the timed launch\'s norm / zcr outputs of {len(idx)} clips: first / middle / '
+                         f'last clip of 4 of the {grid} persistent workgroups + {min(k, n)} seeded '
+                         'random clips; float64 oracle')
+        norm = fe_out[0][idx].cpu().numpy()
+        zc = fe_out[1][idx].cpu().numpy()
+    elif wl == 'od_pipeline':
+        nrm = torch.empty((len(idx), 128, 151), dtype=torch.float32, device='cuda')
+        ctx.od_features_dev(sub.data_ptr(), len(idx), clip_len, clip_len, norm=nrm.data_ptr())
         torch.cuda.synchronize()
-        norm = norm.cpu().numpy()
+        norm = nrm.cpu().numpy()
+        zc = None
+    if wl in ('od_pipeline', 'od_features'):
         feats = [od_fe.od_features(host[j]) for j in range(len(idx))]
         err = 0.0
+        zbad = 0
         for j, f in enumerate(feats):
             ok = ~np.isnan(f['norm'])
             if ok.any():
                 err = max(err, float(np.abs(norm[j][ok] - f['norm'][ok]).max()))
+            if zc is not None:
+                zbad += int(not np.array_equal(np.rint(zc[j] * 400).astype(int),
+                                               np.rint(f['zcr'][0] * 400).astype(int)))
         out['od_norm_logmel_max_abs_err'] = err
+        if zc is not None:
+            out['zcr_count_mismatch_clips'] = zbad
         if wl == 'od_pipeline':
             ref = Nets(W).od_forward(np.stack([f['png_rgb'] for f in feats]).astype(np.float32))
     else:
@@ -365,7 +397,8 @@ def main():
                 err = max(err, float(np.abs(nr_out[i].cpu().numpy() - w).max()))
             parity = {'sample_clips': len(idx), 'nr_max_abs_err_vs_oracle': err}
         else:
-            parity = parity_sample(ctx, wl, pcm, probs, argmax, W, mb, clip_len)
+            parity = parity_sample(ctx, wl, pcm, probs, argmax, W, mb, clip_len,
+                                   fe_out=(norm, zcr) if wl == 'od_features' else None)
 
     # batch-1 latency of the host-pointer call the reference's real-time loop makes (one 2.56 s
     # window per predict, record_on_pc.py:139-160): median of 20 after 5 warmups, outside the

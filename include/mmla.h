@@ -227,6 +227,27 @@ int mmla_vad_collect(mmla_ctx* ctx, const int16_t* pcm, int64_t n_items, int64_t
 int mmla_pcm16(mmla_ctx* ctx, const float* y, int64_t n, int16_t* out, uint32_t flags);
 
 /*
+ * Rate conversion of the offline pre-conditioning (resample.hip).
+ * mmla_ratecv: pydub AudioSegment.set_frame_rate(outrate) on 16-bit PCM, i.e.
+ *   audioop.ratecv(data, 2, nch, inrate, outrate, None) (OverlapDetection/scripts/
+ *   overlap_detection_post_processing.py:120-121; SpeakerIdentification/scripts/
+ *   speaker_identification_post_processing.py:159-160), bit-identical to CPython's audioop.
+ *   pcm [n_frames][nch] interleaved -> out [out_frames][nch]; out_frames must be
+ *   (n_frames - 1) * (outrate / g) / (inrate / g) + 1 with g = gcd(inrate, outrate) (0 for no input).
+ * mmla_resample_sinc: resampy.resample(x, sr_orig, sr_new, filter=<half window>) on one float32
+ *   channel -- librosa.load(path) at its default 22050 Hz uses filter 'kaiser_best'
+ *   (speaker_identification_post_processing.py:142).  half_window [window_len] float64 is the
+ *   filter's right half sampled num_table times per zero crossing (resampy sinc_window); n_out must
+ *   be int(n * sr_new / sr_orig).  resampy's float64 time register, filter interpolation and float32
+ *   accumulation are reproduced (library absent here: parity against resampy itself unpinned).
+ */
+int mmla_ratecv(mmla_ctx* ctx, const int16_t* pcm, int64_t n_frames, int32_t nch, int32_t inrate,
+                int32_t outrate, int16_t* out, int64_t out_frames, uint32_t flags);
+int mmla_resample_sinc(mmla_ctx* ctx, const float* x, int64_t n, int32_t sr_orig, int32_t sr_new,
+                       const double* half_window, int64_t window_len, int32_t num_table, float* y,
+                       int64_t n_out, uint32_t flags);
+
+/*
  * Kernel tracing (replaces the reference's time.time() prints, overlap_detector_run.py:49-104).
  * When enabled, every kernel launch is bracketed by hipEvents on the context stream and its device
  * time is accumulated per stage together with the stage's algorithmic work (bytes for the

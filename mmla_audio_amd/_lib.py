@@ -63,6 +63,8 @@ SIGNATURES = {
     'mmla_vad_remove_silence': [_P, _P, _I64, _I64, _P, _I32, _I64, _P, _P, _P, _I32, _U32],
     'mmla_vad_collect': [_P, _P, _I64, _I64, _P, _I32, _P, _I32, _P, _P, _U32],
     'mmla_pcm16': [_P, _P, _I64, _P, _U32],
+    'mmla_ratecv': [_P, _P, _I64, _I32, _I32, _I32, _P, _I64, _U32],
+    'mmla_resample_sinc': [_P, _P, _I64, _I32, _I32, _P, _I64, _I32, _P, _I64, _U32],
 }
 
 NSTAGES = 7
@@ -280,6 +282,38 @@ class Context:
         self._check(self.lib.mmla_pcm16(self.h, _ptr(a), a.size, _ptr(out), 0), 'mmla_pcm16')
         return out
 
+    # -- rate conversion (offline pre-conditioning) ---------------------------------------------
+    @staticmethod
+    def ratecv_frames(n_frames, inrate, outrate):
+        """output frames of audioop.ratecv(..., state=None) on n_frames input frames"""
+        from math import gcd
+        g = gcd(int(inrate), int(outrate))
+        return (int(n_frames) - 1) * (int(outrate) // g) // (int(inrate) // g) + 1 if n_frames > 0 else 0
+
+    def ratecv(self, pcm, nchannels, inrate, outrate):
+        """audioop.ratecv(pcm, 2, nchannels, inrate, outrate, None)[0] (pydub set_frame_rate) on
+        interleaved int16 frames -> int16 [out_frames * nchannels]"""
+        a = np.ascontiguousarray(pcm, dtype=np.int16).reshape(-1)
+        if a.size % nchannels:
+            raise MmlaError(f'{a.size} samples are not whole frames of {nchannels} channels')
+        nf = a.size // nchannels
+        m = self.ratecv_frames(nf, inrate, outrate)
+        out = np.empty(m * nchannels, np.int16)
+        self._check(self.lib.mmla_ratecv(self.h, _ptr(a), nf, int(nchannels), int(inrate), int(outrate),
+                                         _ptr(out), m, 0), 'mmla_ratecv')
+        return out
+
+    def resample_sinc(self, x, sr_orig, sr_new, half_window, num_table):
+        """resampy.resample(x, sr_orig, sr_new, filter=(half_window, num_table)) on float32 mono"""
+        a = np.ascontiguousarray(x, dtype=np.float32).reshape(-1)
+        w = np.ascontiguousarray(half_window, dtype=np.float64)
+        m = int(a.size * (float(sr_new) / sr_orig))
+        out = np.empty(m, np.float32)
+        self._check(self.lib.mmla_resample_sinc(self.h, _ptr(a), a.size, int(sr_orig), int(sr_new),
+                                                _ptr(w), w.size, int(num_table), _ptr(out), m, 0),
+                    'mmla_resample_sinc')
+        return out
+
     # -- host-array API -----------------------------------------------------------------------
     @staticmethod
     def _pcm(pcm, lens):
@@ -299,13 +333,38 @@ class Context:
         ln = None if lens is None else np.ascontiguousarray(lens, dtype=np.int32)
         return a, ln, a.shape[1]
 
+    @staticmethod
+    def _float_pcm(pcm, lens):
+        """float audio (librosa.load scale: any floating dtype, or a list of float arrays) ->
+        (contiguous float32 [n, L], lens int32 [n] or None, clip_len); None for integer PCM"""
+        if isinstance(pcm, (list, tuple)):
+            if not any(np.issubdtype(np.asarray(p).dtype, np.floating) for p in pcm):
+                return None
+            n = len(pcm)
+            L = max([len(p) for p in pcm] + [1])
+            buf = np.zeros((n, L), np.float32)
+            ln = np.zeros(n, np.int32)
+            for i, p in enumerate(pcm):
+                buf[i, :len(p)] = np.asarray(p, np.float32)
+                ln[i] = len(p)
+            return buf, ln, L
+        a = np.asarray(pcm)
+        if not np.issubdtype(a.dtype, np.floating):
+            return None
+        a = np.ascontiguousarray(a, dtype=np.float32)
+        if a.ndim == 1:
+            a = a[None]
+        ln = None if lens is None else np.ascontiguousarray(lens, dtype=np.int32)
+        return a, ln, a.shape[1]
+
     def od_features(self, pcm, lens=None, db=True, norm=True, zcr=True, img=True):
-        """int16 PCM [n, L] (or a list of 1-D int16 arrays) -> dict of features.  A float32 array
-        (librosa.load scale) goes through mmla_od_features_f32 instead."""
-        if isinstance(pcm, np.ndarray) and pcm.dtype == np.float32:
-            a = np.ascontiguousarray(pcm)[None] if pcm.ndim == 1 else np.ascontiguousarray(pcm)
-            ln = None if lens is None else np.ascontiguousarray(lens, dtype=np.int32)
-            fn, L = self.lib.mmla_od_features_f32, a.shape[1]
+        """int16 PCM [n, L] (or a list of 1-D int16 arrays) -> dict of features.  Float audio
+        (librosa.load scale, any floating dtype or a list of float arrays) goes through
+        mmla_od_features_f32 instead."""
+        fl = self._float_pcm(pcm, lens)
+        if fl is not None:
+            a, ln, L = fl
+            fn = self.lib.mmla_od_features_f32
         else:
             a, ln, L = self._pcm(pcm, lens)
             fn = self.lib.mmla_od_features
@@ -387,6 +446,25 @@ class Context:
         self._check(self.lib.mmla_od_pipeline(self.h, _ptr(sig), n, stride, None, clip_len,
                                               _ptr(probs), _ptr(am), None, 0), 'mmla_od_pipeline')
         return probs, am
+
+    def od_features_strided(self, signal, n, stride, clip_len, db=True, norm=True, zcr=True, img=True):
+        """OD features of n windows of one long signal: window c = signal[c*stride : c*stride +
+        clip_len] (int16 -> mmla_od_features, float -> mmla_od_features_f32; no host copies)"""
+        fl = np.issubdtype(np.asarray(signal).dtype, np.floating)
+        sig = np.ascontiguousarray(signal, dtype=np.float32 if fl else np.int16).reshape(-1)
+        if n < 0 or (n > 0 and (n - 1) * stride + clip_len > sig.size):
+            raise MmlaError(f'{n} windows of {clip_len} at stride {stride} exceed {sig.size} samples')
+        bufs = {}
+        for key, want, shape, dt in (('db', db, (n, OD_MELS, OD_FRAMES), np.float32),
+                                     ('norm', norm, (n, OD_MELS, OD_FRAMES), np.float32),
+                                     ('zcr', zcr, (n, OD_FRAMES), np.float32),
+                                     ('img', img, (n, OD_MELS, OD_FRAMES, 3), np.uint8)):
+            bufs[key] = np.empty(shape, dt) if want else None
+        fn = self.lib.mmla_od_features_f32 if fl else self.lib.mmla_od_features
+        self._check(fn(self.h, _ptr(sig), n, stride, None, clip_len, _ptr(bufs['db']),
+                       _ptr(bufs['norm']), _ptr(bufs['zcr']), _ptr(bufs['img']), 0),
+                    'mmla_od_features(strided)')
+        return {k: v for k, v in bufs.items() if v is not None}
 
     def si_pipeline(self, pcm, lens=None):
         a, ln, L = self._pcm(pcm, lens)

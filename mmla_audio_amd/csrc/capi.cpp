@@ -2,7 +2,9 @@
 // See include/mmla.h for the contract and the reference call site each entry point replaces.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
+#include <numeric>
 #include <cstdarg>
 #include <cstdlib>
 #include <cstdio>
@@ -20,6 +22,7 @@
 #include "si_fe.h"
 #include "nr.h"
 #include "vad.h"
+#include "resample.h"
 
 namespace {
 
@@ -296,7 +299,7 @@ enum Slot {
   S_PCM = 0, S_LENS, S_IMG, S_X, S_T1, S_T2, S_T3, S_SEQ, S_HOUT, S_LOGIT, S_FEAT, S_SILENT,
   S_OUT0, S_OUT1, S_OUT2, S_OUT3, S_IN, S_FESCR,
   S_NR_S, S_NR_BITS, S_NR_FMAX, S_NR_FRAMES, S_NR_ITEMS, S_NR_Y, S_NR_ROWS,
-  S_VAD_SPEECH, S_VAD_OUT, S_VAD_LENS
+  S_VAD_SPEECH, S_VAD_OUT, S_VAD_LENS, S_RS_TR, S_RS_WIN
 };
 
 // ---- weights -------------------------------------------------------------------------------------
@@ -1702,6 +1705,102 @@ int mmla_pcm16(mmla_ctx* c, const float* y, int64_t n, int16_t* out, uint32_t fl
   CHK(out_ptr(c, out, 0, n, dev, S_VAD_OUT, &d));
   LAUNCH(c, MMLA_STAGE_GLUE, (double)n * 6, pcm16_launch(dy, n, d, c->stream));
   CHK(copy_back(c, out, 0, d, n, dev));
+  return finish(c, dev);
+}
+
+// ---- rate conversion of the offline pre-conditioning (resample.hip) ------------------------------
+
+int mmla_ratecv(mmla_ctx* c, const int16_t* pcm, int64_t n_frames, int32_t nch, int32_t inrate,
+                int32_t outrate, int16_t* out, int64_t out_frames, uint32_t flags) {
+  if (!c) return MMLA_E_INVALID;
+  if (n_frames < 0 || nch < 1 || nch > 64 || inrate < 1 || outrate < 1 ||
+      (n_frames > 0 && (!pcm || !out)))
+    return fail(c, MMLA_E_INVALID, "bad ratecv args");
+  const int g = std::gcd(inrate, outrate);
+  const int64_t ir = inrate / g, orr = outrate / g;
+  const int64_t want = n_frames > 0 ? (n_frames - 1) * orr / ir + 1 : 0;
+  if (out_frames != want)
+    return fail(c, MMLA_E_INVALID, "ratecv of %lld frames %d -> %d Hz gives %lld frames, not %lld",
+                (long long)n_frames, inrate, outrate, (long long)want, (long long)out_frames);
+  if (n_frames == 0) return MMLA_OK;
+  HIPCHK(c, hipSetDevice(c->device));
+  const bool dev = flags & MMLA_DEVICE_PTR;
+  const int16_t* din = pcm;
+  if (!dev) {
+    void* p = nullptr;
+    CHK(ws_get(c, S_PCM, (size_t)n_frames * nch * sizeof(int16_t), &p));
+    HIPCHK(c, hipMemcpyAsync(p, pcm, (size_t)n_frames * nch * sizeof(int16_t), hipMemcpyHostToDevice,
+                             c->stream));
+    din = static_cast<const int16_t*>(p);
+  }
+  int16_t* d;
+  CHK(out_ptr(c, out, 0, (size_t)want * nch, dev, S_VAD_OUT, &d));
+  LAUNCH(c, MMLA_STAGE_GLUE, 2.0 * nch * (double)(n_frames + want),
+         ratecv_launch(din, n_frames, nch, (int)ir, (int)orr, d, want, c->stream));
+  CHK(copy_back(c, out, 0, d, (size_t)want * nch, dev));
+  return finish(c, dev);
+}
+
+int mmla_resample_sinc(mmla_ctx* c, const float* x, int64_t n, int32_t sr_orig, int32_t sr_new,
+                       const double* half_window, int64_t window_len, int32_t num_table, float* y,
+                       int64_t n_out, uint32_t flags) {
+  if (!c) return MMLA_E_INVALID;
+  if (n < 0 || sr_orig < 1 || sr_new < 1 || window_len < 2 || num_table < 1 || !half_window ||
+      (n > 0 && (!x || !y)))
+    return fail(c, MMLA_E_INVALID, "bad resample args");
+  const double ratio = (double)sr_new / (double)sr_orig;
+  const int64_t want = (int64_t)((double)n * ratio);      // resampy: int(n * sample_ratio)
+  if (n_out != want)
+    return fail(c, MMLA_E_INVALID, "resampling %lld samples %d -> %d Hz gives %lld, not %lld",
+                (long long)n, sr_orig, sr_new, (long long)want, (long long)n_out);
+  if (n_out == 0) return MMLA_OK;
+  const double scale = std::min(1.0, ratio);
+  const int index_step = (int)(scale * num_table);
+  if (index_step < 1) return fail(c, MMLA_E_INVALID, "ratio %g too small for the filter table", ratio);
+  HIPCHK(c, hipSetDevice(c->device));
+  const bool dev = flags & MMLA_DEVICE_PTR;
+  // the filter as resampy prepares it: scaled by the ratio when downsampling, then its forward
+  // difference (last entry 0), interleaved (win, delta) for one 16-B load per tap
+  std::vector<double> wd(2 * window_len);
+  for (int64_t i = 0; i < window_len; ++i) wd[2 * i] = ratio < 1 ? half_window[i] * ratio : half_window[i];
+  for (int64_t i = 0; i < window_len; ++i)
+    wd[2 * i + 1] = i + 1 < window_len ? wd[2 * i + 2] - wd[2 * i] : 0.0;
+  // the time register of the sequential loop: repeated float64 addition of 1 / ratio
+  std::vector<double> tr(n_out);
+  const double inc = 1.0 / ratio;
+  double t_reg = 0.0;
+  for (int64_t t = 0; t < n_out; ++t) {
+    tr[t] = t_reg;
+    t_reg += inc;
+  }
+  void *ptr = nullptr, *pw = nullptr;
+  CHK(ws_get(c, S_RS_TR, (size_t)n_out * sizeof(double), &ptr));
+  CHK(ws_get(c, S_RS_WIN, wd.size() * sizeof(double), &pw));
+  HIPCHK(c, hipMemcpyAsync(ptr, tr.data(), (size_t)n_out * sizeof(double), hipMemcpyHostToDevice,
+                           c->stream));
+  HIPCHK(c, hipMemcpyAsync(pw, wd.data(), wd.size() * sizeof(double), hipMemcpyHostToDevice, c->stream));
+  const float* dx = x;
+  if (!dev) {
+    void* p = nullptr;
+    CHK(ws_get(c, S_IN, (size_t)n * sizeof(float), &p));
+    HIPCHK(c, hipMemcpyAsync(p, x, (size_t)n * sizeof(float), hipMemcpyHostToDevice, c->stream));
+    dx = static_cast<const float*>(p);
+  }
+  SincResampleArgs a{};
+  a.x = dx;
+  a.n_orig = n;
+  a.tr = static_cast<const double*>(ptr);
+  a.win = static_cast<const double*>(pw);
+  a.nwin = window_len;
+  a.num_table = num_table;
+  a.index_step = index_step;
+  a.scale = scale;
+  a.n_out = n_out;
+  CHK(out_ptr(c, y, 0, (size_t)n_out, dev, S_OUT0, &a.y));
+  LAUNCH(c, MMLA_STAGE_GLUE, 4.0 * (double)(n + n_out), sinc_resample_launch(a, c->stream));
+  CHK(copy_back(c, y, 0, a.y, (size_t)n_out, dev));
+  // the host vectors above are read by the async uploads: wait before they go out of scope
+  HIPCHK(c, hipStreamSynchronize(c->stream));
   return finish(c, dev);
 }
 

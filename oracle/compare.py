@@ -48,3 +48,41 @@ def argmax_report(p, ref):
 
 def argmax_ok(p, ref):
     return argmax_report(p, ref)[1] == 0
+
+
+# OD front-end bars: normalised log-mel <= 1e-4, dB <= 5e-3, exact crossing counts,
+# image R exact and G/B <= 1 LSB (on <= 1e-4 of the pixel values of a test: od_lsb_budget)
+OD_NORM_TOL = 1e-4
+OD_DB_TOL = 5e-3
+
+
+def od_clip_compare(f, i, ref, tag):
+    """clip i of a GPU feature dict f (keys present of db / norm / zcr / img) against the oracle's
+    od_features(...) dict; -> (pixel values 1 LSB off, pixel values) for od_lsb_budget"""
+    nan = np.isnan(ref['norm'])
+    if 'norm' in f:
+        assert np.array_equal(np.isnan(f['norm'][i]), nan), tag
+        if (~nan).any():
+            err = np.abs(f['norm'][i][~nan] - ref['norm'][~nan]).max()
+            assert err <= OD_NORM_TOL, f'{tag}: norm err {err}'
+    if 'db' in f and (~nan).any():
+        derr = np.abs(f['db'][i] - ref['db']).max()
+        assert derr <= OD_DB_TOL, f'{tag}: dB err {derr}'
+    if 'zcr' in f:
+        counts = np.rint(f['zcr'][i] * 400).astype(int)
+        assert np.array_equal(counts, np.rint(ref['zcr'][0] * 400).astype(int)), tag
+        assert np.abs(f['zcr'][i] - ref['zcr'][0]).max() < 1e-7
+    if 'img' not in f:
+        return 0, 0
+    img = f['img'][i].astype(int)
+    want = ref['png_rgb'].astype(int)
+    assert np.array_equal(img[..., 0], want[..., 0]), f'{tag}: R channel'
+    d = np.abs(img - want)
+    assert d.max() <= 1, f'{tag}: {d.max()} LSB'
+    return np.count_nonzero(d), d.size
+
+
+def od_lsb_budget(counts):
+    """<= 1 LSB on <= 1e-4 of the pixel values, over all clips of a test"""
+    off, tot = np.sum(np.asarray(counts, np.int64).reshape(-1, 2), axis=0)
+    assert off <= 1e-4 * max(tot, 1), f'{off} of {tot} pixel values 1 LSB off'

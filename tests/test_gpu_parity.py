@@ -25,28 +25,11 @@ def ctx():
 
 
 def _od_compare(f, i, ref, tag):
-    nan = np.isnan(ref['norm'])
-    assert np.array_equal(np.isnan(f['norm'][i]), nan), tag
-    if (~nan).any():
-        err = np.abs(f['norm'][i][~nan] - ref['norm'][~nan]).max()
-        assert err <= 1e-4, f'{tag}: norm err {err}'
-        derr = np.abs(f['db'][i] - ref['db']).max()
-        assert derr <= 5e-3, f'{tag}: dB err {derr}'
-    counts = np.rint(f['zcr'][i] * 400).astype(int)
-    assert np.array_equal(counts, np.rint(ref['zcr'][0] * 400).astype(int)), tag
-    assert np.abs(f['zcr'][i] - ref['zcr'][0]).max() < 1e-7
-    img = f['img'][i].astype(int)
-    want = ref['png_rgb'].astype(int)
-    assert np.array_equal(img[..., 0], want[..., 0]), f'{tag}: R channel'
-    d = np.abs(img - want)
-    assert d.max() <= 1, f'{tag}: {d.max()} LSB'
-    return np.count_nonzero(d), d.size
+    return compare.od_clip_compare(f, i, ref, tag)
 
 
 def _lsb_budget(counts):
-    """<= 1 LSB on <= 1e-4 of the pixel values, over all clips of a test"""
-    off, tot = np.sum(counts, axis=0)
-    assert off <= 1e-4 * tot, f'{off} of {tot} pixel values 1 LSB off'
+    compare.od_lsb_budget(counts)
 
 
 def test_od_features_golden(ctx, od_golden):
