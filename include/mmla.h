@@ -76,10 +76,12 @@ int mmla_synchronize(mmla_ctx* ctx);
  *   MMLA_PREC_F16X3 (default) error-compensated 3xFP16 on f16 MFMA: operands split hi + 2^-11 lo,
  *                   hi*hi + hi*lo + lo*hi accumulated in f32 (~22-bit products, f32 accumulation);
  *                   needs |activations| < 65504 in the fused res_blocks, < 4094 in the halo-tiled
- *                   convs (split x 2^4) and < 1023 in the LSTM (x 2^6); |weights| < 255.9 (x 2^8).
- *                   Range guard: weights outside it make that model run exact f32 (decided at
- *                   mmla_load_weights); every kernel that splits an activation flags a value
- *                   outside it.  Host-pointer calls then re-run the micro-batch in exact f32
+ *                   convs (split x 2^4) and < 1023 in the LSTM (x 2^6).  Each weight tensor is split
+ *                   at its own power-of-two scale (2^8 for max |w| in [1/16, 255.9), else the one
+ *                   putting max |w| in [2^13, 2^14)), so any finite checkpoint stays on this path;
+ *                   a tensor holding inf / NaN makes that model run exact f32 (decided at
+ *                   mmla_load_weights).  Range guard: every kernel that splits an activation flags
+ *                   a value outside its range.  Host-pointer calls then re-run the micro-batch in exact f32
  *                   (counted by mmla_range_check); device-pointer calls report MMLA_E_RANGE from
  *                   the next mmla_range_check / mmla_synchronize.
  *   MMLA_PREC_F32   exact f32 MFMA (v_mfma_f32_32x32x2_f32), 1/5.3 of the throughput.

@@ -41,6 +41,8 @@ struct ConvW {
   uint16_t* fh = nullptr;   // fused res_block layout [cout][kpad], k = tap * cin + ci (resblk.hip)
   uint16_t* fl = nullptr;
   int kh = 0, kw = 0, cin = 0, cout = 0, cout_pad = 0, cin_pad = 0, kpad = 0;
+  float wscale = 256.0f;    // power-of-two scale of the fp16 hi/lo split (pick_wscale)
+  float unscale() const { return 1.0f / (16.0f * wscale); }   // x the 2^4 activation scale
 };
 struct BnW {
   float* scale = nullptr;
@@ -52,6 +54,7 @@ struct LstmW {
   float* bias[2] = {nullptr, nullptr};
   uint16_t* wth[2] = {nullptr, nullptr};   // 3xFP16 split, transposed [1024][256 + D] (nets.hip)
   uint16_t* wtl[2] = {nullptr, nullptr};
+  float ws[2] = {256.0f, 256.0f};          // per-direction split scale (pick_wscale)
 };
 struct OdBlock {
   BnW bn_in, bn_mid;
@@ -329,14 +332,34 @@ int upload(mmla_ctx* c, std::vector<void*>& allocs, const void* host, size_t byt
   return MMLA_OK;
 }
 
+// The power-of-two scale at which a weight tensor is split into fp16 hi + lo for the 3xFP16 MFMA
+// paths (one fixed 2^8 sent a whole model to exact f32 as soon as one weight
+// reached 255.9).  2^8 for the usual max |w| in [1/16, 255.9) -- the arithmetic of earlier rounds,
+// bit for bit -- else the scale that puts max |w| in [2^13, 2^14): far from the fp16 overflow and
+// with the lo halves of the large weights normal.  The kernels multiply by its inverse (exact).
+// false in *finite for a tensor holding inf / NaN (that model runs exact f32).
+static float pick_wscale(const float* w, size_t n, bool* finite) {
+  float m = 0.0f;
+  *finite = true;
+  for (size_t i = 0; i < n; ++i) {
+    const float a = std::fabs(w[i]);
+    if (!(a <= 3.4e38f)) *finite = false;
+    else m = std::max(m, a);
+  }
+  if (m == 0.0f || (m < 255.9f && m >= 0.0625f)) return 256.0f;
+  const int e = std::max(-100, std::min(100, (int)std::floor(std::log2(16384.0 / m))));
+  return std::ldexp(1.0f, e);
+}
+
 int take_conv(mmla_ctx* c, Cursor& cur, std::vector<void*>& al, int kh, int kw, int cin, int cout,
               ConvW* w) {
   const float* k = cur.take((int64_t)kh * kw * cin * cout);
   const float* b = cur.take(cout);
   if (!cur.ok) return fail(c, MMLA_E_SHAPE, "weight blob too short");
-  // 3xFP16 needs fp16-range weights: conv_h3 splits w * 2^8 (conv_h3.hip), so |w| < 65504 / 2^8
-  for (int64_t i = 0; i < (int64_t)kh * kw * cin * cout; ++i)
-    if (!(std::fabs(k[i]) < 65504.0f / 256.0f)) c->loading_f16_bad = true;
+  // 3xFP16: any finite tensor fits the fp16 split at its own power-of-two scale
+  bool finite = true;
+  w->wscale = pick_wscale(k, (size_t)kh * kw * cin * cout, &finite);
+  if (!finite) c->loading_f16_bad = true;
   w->kh = kh;
   w->kw = kw;
   w->cin = cin;
@@ -356,7 +379,8 @@ int take_conv(mmla_ctx* c, Cursor& cur, std::vector<void*>& al, int kh, int kw, 
     w->cin_pad = (cin + 15) / 16 * 16;
     const size_t n = (size_t)kh * kw * w->cout_pad * w->cin_pad;
     std::vector<uint16_t> hi(n), lo(n);
-    conv_h3_split_weights(k, kh, kw, cin, cout, w->cin_pad, w->cout_pad, hi.data(), lo.data());
+    conv_h3_split_weights(k, kh, kw, cin, cout, w->cin_pad, w->cout_pad, hi.data(), lo.data(),
+                          w->wscale);
     float* p = nullptr;
     CHK(upload(c, al, hi.data(), n * sizeof(uint16_t), &p));
     w->wh = reinterpret_cast<uint16_t*>(p);
@@ -369,7 +393,7 @@ int take_conv(mmla_ctx* c, Cursor& cur, std::vector<void*>& al, int kh, int kw, 
     std::vector<uint16_t> hi(n), lo(n);
     // the 3x3 (GEMM 1) and conv(4,1) (GEMM 2) weights in MFMA fragment order; the 1x1 shortcut
     // keeps [co][k] rows
-    resblk_split_weights(k, kh * kw, cin, cout, w->kpad, hi.data(), lo.data(), kh > 1);
+    resblk_split_weights(k, kh * kw, cin, cout, w->kpad, hi.data(), lo.data(), kh > 1, w->wscale);
     float* p = nullptr;
     CHK(upload(c, al, hi.data(), n * sizeof(uint16_t), &p));
     w->fh = reinterpret_cast<uint16_t*>(p);
@@ -408,9 +432,11 @@ int take_lstm(mmla_ctx* c, Cursor& cur, std::vector<void*>& al, int d, LstmW* l)
     memcpy(wc.data() + 256 * 1024, k, sizeof(float) * d * 1024);
     CHK(upload(c, al, wc.data(), wc.size() * sizeof(float), &l->wcat[dir]));
     CHK(upload(c, al, b, 1024 * sizeof(float), &l->bias[dir]));
-    if (!bilstm_h3_weights_in_range(wc.data(), d)) c->loading_f16_bad = true;
+    bool finite = true;
+    l->ws[dir] = pick_wscale(wc.data(), wc.size(), &finite);
+    if (!finite) c->loading_f16_bad = true;
     std::vector<uint16_t> hi(wc.size()), lo(wc.size());
-    bilstm_h3_split_weights(wc.data(), d, hi.data(), lo.data());
+    bilstm_h3_split_weights(wc.data(), d, hi.data(), lo.data(), l->ws[dir]);
     float* p = nullptr;
     CHK(upload(c, al, hi.data(), hi.size() * sizeof(uint16_t), &p));
     l->wth[dir] = reinterpret_cast<uint16_t*>(p);
@@ -644,6 +670,7 @@ int conv_spatial(mmla_ctx* c, const ConvW& w, const float* x, float* y, int n, i
       a.sc_bias = sc->bias;
       a.sc_cin = sc->cin;
       a.sc_h = sc_h;
+      a.sc_unscale = sc->unscale();
       // pooled 2-D blocks: one output per pooled pixel; Conv1D: one per output row (h = rows)
       sc_flops = sc_h > 0 ? 2.0 * n * h * sc->cin * sc->cout
                           : 2.0 * n * ((h + 1) / 2) * ((wd + 1) / 2) * sc->cin * sc->cout;
@@ -653,6 +680,7 @@ int conv_spatial(mmla_ctx* c, const ConvW& w, const float* x, float* y, int n, i
     a.x = x;
     a.wh = w.wh;
     a.wl = w.wl;
+    a.unscale = w.unscale();
     a.bias = w.bias;
     a.scale = bn ? bn->scale : nullptr;
     a.shift = bn ? bn->shift : nullptr;
@@ -688,7 +716,7 @@ double lstm_flops(int64_t n, int T, int D) { return 2.0 * n * T * 2 * (256.0 + D
 hipError_t lstm_run(mmla_ctx* c, const LstmW& L, const float* seq, int64_t n, int T, float* out) {
   if (c->precision == MMLA_PREC_F16X3 && L.wth[0])
     return bilstm_h3_launch(seq, (int)n, T, 128, L.wth[0], L.wtl[0], L.wth[1], L.wtl[1], L.bias[0],
-                            L.bias[1], out, c->range_ptr, c->stream);
+                            L.bias[1], out, c->range_ptr, L.ws[0], L.ws[1], c->stream);
   return bilstm_launch(seq, (int)n, T, 128, L.wcat[0], L.wcat[1], L.bias[0], L.bias[1], out,
                        c->stream);
 }
@@ -744,6 +772,9 @@ int run_od_net(mmla_ctx* c, const uint8_t* img_u8, const float* img_f32, int64_t
       r.w1h = B.c3.fh;
       r.w1l = B.c3.fl;
       r.b1 = B.c3.bias;
+      r.u1 = B.c3.unscale();
+      r.u2 = B.c4.unscale();
+      r.us = POOL[b] ? B.sc.unscale() : 0.0f;
       r.s1 = B.bn_in.scale;
       r.t1 = B.bn_in.shift;
       r.w2h = B.c4.fh;
@@ -905,6 +936,7 @@ int run_si_net(mmla_ctx* c, const float* x, int64_t n, float* probs, int32_t* ar
     a.x = static_cast<float*>(ph);
     a.wh = W.dense.wh;
     a.wl = W.dense.wl;
+    a.unscale = W.dense.unscale();
     a.bias = W.dense.bias;
     a.y = static_cast<float*>(pl);
     a.n = (int)n;

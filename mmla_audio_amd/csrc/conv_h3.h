@@ -32,6 +32,10 @@ struct ConvH3Args {
   const float* sc_bias;  // [cout_pad]
   int sc_cin;            // multiple of 16
   int sc_h;              // Conv1D: input rows per clip
+  // 1 / (2^4 activation scale x the power-of-two weight scale of conv_h3_split_weights): per weight
+  // tensor, so that any finite checkpoint fits the fp16 split (capi.cpp pick_wscale)
+  float unscale;
+  float sc_unscale;
 };
 
 // Picks the tile and launches; returns hipErrorInvalidValue for unsupported shapes.
@@ -39,4 +43,4 @@ hipError_t conv_h3_launch(ConvH3Args a, hipStream_t stream);
 // Host: split float32 weights [kh,kw,cin,cout] into fp16 hi/lo, per tap in MFMA fragment order
 // [cin_pad / 16][cout_pad / 32][64 lanes][8] (conv_h3_kernel).
 void conv_h3_split_weights(const float* w, int kh, int kw, int cin, int cout, int cin_pad,
-                           int cout_pad, uint16_t* hi, uint16_t* lo);
+                           int cout_pad, uint16_t* hi, uint16_t* lo, float wscale);

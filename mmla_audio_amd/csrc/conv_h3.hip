@@ -53,8 +53,8 @@ typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 constexpr int NT = 256;
 constexpr int BM = 128;
 constexpr float ACT_SCALE = 16.0f;      // 2^4: staged activations
-constexpr float W_SCALE = 256.0f;       // 2^8: weights (conv_h3_split_weights)
-constexpr float UNSCALE = 1.0f / (ACT_SCALE * W_SCALE);
+// weights are split at a per-tensor power-of-two scale (conv_h3_split_weights, capi.cpp pick_wscale:
+// 2^8 for the usual |w| in [1/16, 255.9)); the epilogue multiplies by a.unscale = 2^-4 / that scale
 constexpr float ACT_RANGE = 65504.0f / ACT_SCALE;   // largest finite fp16 / the activation scale
 
 template <int PRO>
@@ -496,10 +496,10 @@ __global__ void __launch_bounds__(NT, (conv_minw<KH, BN, TW, EPI, SHP::FIXED>())
         for (int g = 0; g < 4; ++g) {
           const int co = n0 + (wn * NTL + nt) * 32 + 8 * g + cq;
           if (co >= A_COUT) continue;
-          float4 v = make_float4(fmaf(acc[mt][nt][4 * g], UNSCALE, b4[g].x),
-                                 fmaf(acc[mt][nt][4 * g + 1], UNSCALE, b4[g].y),
-                                 fmaf(acc[mt][nt][4 * g + 2], UNSCALE, b4[g].z),
-                                 fmaf(acc[mt][nt][4 * g + 3], UNSCALE, b4[g].w));
+          float4 v = make_float4(fmaf(acc[mt][nt][4 * g], a.unscale, b4[g].x),
+                                 fmaf(acc[mt][nt][4 * g + 1], a.unscale, b4[g].y),
+                                 fmaf(acc[mt][nt][4 * g + 2], a.unscale, b4[g].z),
+                                 fmaf(acc[mt][nt][4 * g + 3], a.unscale, b4[g].w));
           if constexpr (ADD) {
             const float4 r = rsd4[nt][mt][g];
             v = make_float4(v.x + r.x, v.y + r.y, v.z + r.z, v.w + r.w);
@@ -626,7 +626,7 @@ __global__ void __launch_bounds__(NT, (conv_minw<KH, BN, TW, EPI, SHP::FIXED>())
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-          for (int i = 0; i < 16; ++i) rsd[nt][mt][i] = fmaf(sacc[nt][mt][i], UNSCALE, bsc);
+          for (int i = 0; i < 16; ++i) rsd[nt][mt][i] = fmaf(sacc[nt][mt][i], a.sc_unscale, bsc);
       }
     }
   }
@@ -669,7 +669,7 @@ __global__ void __launch_bounds__(NT, (conv_minw<KH, BN, TW, EPI, SHP::FIXED>())
     for (int mt = 0; mt < MT; ++mt) {
       float v[16];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) v[r] = fmaf(acc[mt][nt][r], UNSCALE, b);
+      for (int r = 0; r < 16; ++r) v[r] = fmaf(acc[mt][nt][r], a.unscale, b);
       const int mbase = (wm * MT + mt) * 32;
       if constexpr (POOL) {
         // windows: top-left rows i = 8q + hsel + e (i % TW even, (i / TW) even) -> registers
@@ -699,7 +699,7 @@ __global__ void __launch_bounds__(NT, (conv_minw<KH, BN, TW, EPI, SHP::FIXED>())
               if (ow + 1 < A_W) mx = fmaxf(mx, v[4 * q + e + R + 1]);
             }
             // Add()([MaxPool2D(t2), shortcut]): the shortcut's bias added in its own rounding step
-            if (has_sc) mx += fmaf(sacc[nt][4 * mt + jr], UNSCALE, bsc);
+            if (has_sc) mx += fmaf(sacc[nt][4 * mt + jr], a.sc_unscale, bsc);
             a.y[((clip * hp + (oh >> 1)) * wp + (ow >> 1)) * A_COUT + co] = mx;
           }
       } else {
@@ -876,13 +876,13 @@ static uint16_t f32_to_f16_bits(float f) {
 }
 
 void conv_h3_split_weights(const float* w, int kh, int kw, int cin, int cout, int cin_pad,
-                           int cout_pad, uint16_t* hi, uint16_t* lo) {
+                           int cout_pad, uint16_t* hi, uint16_t* lo, float wscale) {
   const size_t n = (size_t)kh * kw * cout_pad * cin_pad;
   for (size_t i = 0; i < n; ++i) hi[i] = lo[i] = 0;
   for (int t = 0; t < kh * kw; ++t)
     for (int ci = 0; ci < cin; ++ci)
       for (int co = 0; co < cout; ++co) {
-        const float v = w[((size_t)t * cin + ci) * cout + co] * W_SCALE;   // exact
+        const float v = w[((size_t)t * cin + ci) * cout + co] * wscale;   // exact (power of two)
         const _Float16 h = (_Float16)v;
         // MFMA fragment order: [tap][ci / 16][co / 32][lane = co % 32 + 32 (ci % 16 / 8)][ci % 8]
         const size_t o = (size_t)t * cout_pad * cin_pad +

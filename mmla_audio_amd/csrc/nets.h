@@ -25,10 +25,10 @@ hipError_t bilstm_launch(const float* seq, int n, int T, int D, const float* wca
 hipError_t bilstm_h3_launch(const float* seq, int n, int T, int D, const uint16_t* wfh,
                             const uint16_t* wfl, const uint16_t* wbh, const uint16_t* wbl,
                             const float* bias_fwd, const float* bias_bwd, float* out,
-                            int* range_flag /*nullable: set when |x| >= 65504 / 64*/, hipStream_t s);
-void bilstm_h3_split_weights(const float* wcat, int D, uint16_t* hi, uint16_t* lo);
-// The kernel scales the weights by 2^8 before the fp16 split: false when max |w| * 256 >= 65504.
-bool bilstm_h3_weights_in_range(const float* wcat, int D);
+                            int* range_flag /*nullable: set when |x| >= 65504 / 64*/,
+                            float ws_fwd, float ws_bwd, hipStream_t s);
+// split at the direction's power-of-two weight scale ws (the kernel's ws_fwd / ws_bwd)
+void bilstm_h3_split_weights(const float* wcat, int D, uint16_t* hi, uint16_t* lo, float ws);
 // OD head: LeakyReLU(0.3) -> Dense(512 -> 2) -> softmax; probs [n,2], argmax [n] (nullable).
 // The 'silent' gate of record_on_pc.py:141-154: with clip_len >= 0, clips with fewer than 4000
 // samples (lens[i], or clip_len when lens is null) get argmax -1 and silent[i] = 1 (nullable).

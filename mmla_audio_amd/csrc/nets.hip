@@ -190,9 +190,8 @@ typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 MMLA_DEV float sigm_f(float z) { return __frcp_rn(1.0f + __expf(-z)); }
 MMLA_DEV float tanh_f(float x) { return 1.0f - 2.0f * __frcp_rn(1.0f + __expf(2.0f * x)); }
 
-constexpr float LSTM_WS = 256.0f;   // weight scale (bilstm_h3_split_weights)
+// weights: a per-direction power-of-two scale ws (bilstm_h3_split_weights; capi.cpp pick_wscale)
 constexpr float LSTM_AS = 64.0f;    // [h | x] scale
-constexpr float LSTM_UNSCALE = 1.0f / (LSTM_WS * LSTM_AS);
 
 MMLA_DEV void split1(float v, _Float16& h, _Float16& l) {   // v * 2^6 = hi + lo
   v *= LSTM_AS;
@@ -211,7 +210,8 @@ __global__ void __launch_bounds__(512) bilstm_h3_kernel(const float* __restrict_
                                                         const float* __restrict__ bf,
                                                         const float* __restrict__ bb,
                                                         float* __restrict__ out,
-                                                        int* __restrict__ range_flag) {
+                                                        int* __restrict__ range_flag, float ws_f,
+                                                        float ws_b) {
   constexpr int K = LSTM_U + D;          // 384
   constexpr int KST = K / 16;            // k-steps
   constexpr int LDA = K + 8;             // fp16 per A row (16-B pad)
@@ -225,6 +225,8 @@ __global__ void __launch_bounds__(512) bilstm_h3_kernel(const float* __restrict_
   const uint16_t* __restrict__ Wh = dir == 0 ? wfh : wbh;
   const uint16_t* __restrict__ Wl = dir == 0 ? wfl : wbl;
   const float* __restrict__ B = dir == 0 ? bf : bb;
+  const float WS = dir == 0 ? ws_f : ws_b;
+  const float LSTM_UNSCALE = 1.0f / (WS * LSTM_AS);   // exact: powers of two
   const int64_t c0 = (int64_t)blockIdx.x * ROWS;
 
   for (int e = tid; e < ROWS * LSTM_U; e += NTH) {   // h_{-1} = 0
@@ -282,7 +284,7 @@ __global__ void __launch_bounds__(512) bilstm_h3_kernel(const float* __restrict_
     f32x16 acc[MT][4];
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
-      const float bv = B[g * LSTM_U + col] * (LSTM_WS * LSTM_AS);
+      const float bv = B[g * LSTM_U + col] * (WS * LSTM_AS);
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
@@ -472,30 +474,24 @@ hipError_t bilstm_launch(const float* seq, int n, int T, int D, const float* wf,
 hipError_t bilstm_h3_launch(const float* seq, int n, int T, int D, const uint16_t* wfh,
                             const uint16_t* wfl, const uint16_t* wbh, const uint16_t* wbl,
                             const float* bf, const float* bb, float* out, int* range_flag,
-                            hipStream_t s) {
+                            float ws_fwd, float ws_bwd, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   if (D != 128) return hipErrorInvalidValue;
   // (MT 2 -- 64 clips per workgroup, half the weight stream per clip -- needs ~290 registers per
   // lane: spills at two waves per SIMD, so one 32-clip tile)
   hipLaunchKernelGGL((bilstm_h3_kernel<128, 1>), dim3(blocks_for(n, LSTM_ROWS), 2), dim3(512), 0, s,
-                     seq, n, T, wfh, wfl, wbh, wbl, bf, bb, out, range_flag);
+                     seq, n, T, wfh, wfl, wbh, wbl, bf, bb, out, range_flag, ws_fwd, ws_bwd);
   return hipGetLastError();
 }
 
-bool bilstm_h3_weights_in_range(const float* wcat, int D) {
-  for (size_t i = 0; i < (size_t)(256 + D) * 1024; ++i)
-    if (!(fabsf(wcat[i]) * LSTM_WS < 65504.0f)) return false;   // also inf / NaN
-  return true;
-}
-
-void bilstm_h3_split_weights(const float* wcat, int D, uint16_t* hi, uint16_t* lo) {
+void bilstm_h3_split_weights(const float* wcat, int D, uint16_t* hi, uint16_t* lo, float ws) {
   // MFMA fragment order: gate column j = 256 g + 32 w + n (w: the wave owning it), k = 16 ks + 8 hf +
   // e -> ((g * 8 + w) * KST + ks) * 512 + (n + 32 hf) * 8 + e, i.e. the B fragment of lane
   // n + 32 hf for that gate / wave / k-step (bilstm_h3_kernel)
   const int K = 256 + D, KST = K / 16;
   for (int j = 0; j < 1024; ++j)
     for (int k = 0; k < K; ++k) {
-      const float v = wcat[(size_t)k * 1024 + j] * LSTM_WS;   // exact power-of-two scale
+      const float v = wcat[(size_t)k * 1024 + j] * ws;   // exact power-of-two scale
       const _Float16 h = (_Float16)v;
       const _Float16 l = (_Float16)(v - (float)h);   // not rescaled (bilstm_h3_kernel)
       const int g = j / 256, w = (j % 256) / 32, n = j % 32;

@@ -671,7 +671,8 @@ typedef uint16_t us2 __attribute__((ext_vector_type(2)));
 #define FE3_PRIO 0
 #endif
 #ifndef FE3_SKIP
-#define FE3_SKIP 0   // dev timing builds only: 1 staging, 2 stage 1, 4 stage 2, 8 mel, 16 norm stores skipped
+#define FE3_SKIP 0   // dev timing builds only: 1 staging, 2 stage 1, 4 stage 2, 8 mel, 16 norm stores skipped;
+                     // 32 / 64 / 128: the mel / stage-1 / stage-2 MFMAs replaced by one VALU op each
 #endif
 constexpr int NWV = FE3_NWV;                  // waves per workgroup (one workgroup per CU)
 constexpr int NTH = 64 * NWV;
@@ -1057,6 +1058,10 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
           bl[i] = __builtin_amdgcn_perm(w[2 * i + 1], w[2 * i], 0x07060302u);
         }
         const f16x8 BH = __builtin_bit_cast(f16x8, bh), BL = __builtin_bit_cast(f16x8, bl);
+        if constexpr (FE3_SKIP & 64) {   // dev: stage 1 without its MFMAs (operands still consumed)
+          acc[g][s] += (float)(BH[0] + BL[1]) + (float)a1h[g][s][0];
+          continue;
+        }
         acc[g] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1l[g][s], BH, acc[g], 0, 0, 0);
         acc[g] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1h[g][s], BL, acc[g], 0, 0, 0);
         acc[g] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1h[g][s], BH, acc[g], 0, 0, 0);
@@ -1104,6 +1109,10 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
         const uint2 h0 = zh[4 * s], h1 = zh[4 * s + 1], l0 = zl[4 * s], l1 = zl[4 * s + 1];
         const f16x8 BH = __builtin_bit_cast(f16x8, uint4{h0.x, h0.y, h1.x, h1.y});
         const f16x8 BL = __builtin_bit_cast(f16x8, uint4{l0.x, l0.y, l1.x, l1.y});
+        if constexpr (FE3_SKIP & 128) {   // dev: stage 2 without its MFMAs (operands still consumed)
+          acc[s] += (float)(BH[0] + BL[1]) + (float)a2h[j][s][0];
+          continue;
+        }
         acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a2l[j][s], BH, acc, 0, 0, 0);
         acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a2h[j][s], BL, acc, 0, 0, 0);
         acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a2h[j][s], BH, acc, 0, 0, 0);
@@ -1181,7 +1190,10 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
         bv[j] = pb[4 * PP * (j0 + j)];
       }
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j], bv[j], acc, 0, 0, 0);
+      for (int j = 0; j < 4; ++j) {
+        if constexpr (FE3_SKIP & 32) acc[j] = fmaf(av[j], bv[j], acc[j]);   // dev: the MFMA's cost alone
+        else acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j], bv[j], acc, 0, 0, 0);
+      }
     }
     const bool live = TF * t + TF <= NF || TF * t + 16 * m_fh + (l & 15) < NF;
 #pragma unroll
@@ -1385,6 +1397,10 @@ bool od_fe_tables_ok(const OdFeTables& t) {
   return true;
 }
 
+#ifndef OD_FE_V2_AB
+#define OD_FE_V2_AB 0
+#endif
+#if OD_FE_V2_AB
 template <int NW>
 static void launch_nw(const OdFeArgs& a, int64_t n, hipStream_t s) {
   const dim3 g((unsigned)n), b(NT * NW);
@@ -1405,14 +1421,20 @@ static void launch_v2(const OdFeArgs& a, int64_t n, hipStream_t s) {
   if (n <= v2::NW4_MAX_CLIPS) launch_nw<4>(a, n, s);
   else launch_nw<2>(a, n, s);
 }
+#endif
 
-// v2 (VALU FFT + HBM scratch) stays selectable for A/B measurements: MMLA_OD_FE_V2=1
+// v2 (VALU FFT + HBM scratch) is not in the product build: a dev A/B build
+// (make variant VSRC=od_fe VDEF="-DOD_FE_V2_AB=1 ...") selects it with MMLA_OD_FE_V2=1
 static bool use_v2() {
+#if OD_FE_V2_AB
   static const bool v = [] {
     const char* e = getenv("MMLA_OD_FE_V2");
     return e && e[0] == '1';
   }();
   return v;
+#else
+  return false;
+#endif
 }
 
 bool od_fe_needs_scratch() { return use_v2(); }
@@ -1442,12 +1464,14 @@ static void launch_v3(const OdFeArgs& a, int64_t n, hipStream_t s) {
 
 hipError_t od_fe_launch(const OdFeArgs& a, int64_t n_clips, hipStream_t stream) {
   if (n_clips <= 0) return hipSuccess;
+#if OD_FE_V2_AB
   if (use_v2()) {
     if (!a.scratch || a.pcm_f32) return hipErrorInvalidValue;
     launch_v2(a, n_clips, stream);
-  } else {
-    launch_v3(a, n_clips, stream);
+    return hipGetLastError();
   }
+#endif
+  launch_v3(a, n_clips, stream);
   return hipGetLastError();
 }
 

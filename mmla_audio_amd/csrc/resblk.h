@@ -27,6 +27,8 @@ struct ResBlkArgs {
   int n, h, w;             //   = MaxPool2D(2, 'same')(conv) + Conv2D(1x1, stride 2)(x)
   int tiles_h, tiles_w;    // set by resblk_launch
   int* range_flag;         // nullable: set to 1 when an operand split into fp16 is >= 65504 / inf
+  // 1 / (2^4 x the power-of-two weight scale) of GEMM 1 (w1), GEMM 2 (w2) and the shortcut (ws)
+  float u1, u2, us;
 };
 
 // K of the 3x3 conv padded to the MFMA k-step (32).
@@ -38,4 +40,4 @@ hipError_t resblk_launch(ResBlkArgs a, int cin, int c, bool pool, hipStream_t st
 // (zero for k >= taps * cin); frag: the 16x16x32 MFMA B-fragment order [k / 32][cout / 16][64 lanes][8]
 // (GEMM 1's 3x3 and GEMM 2's conv(4,1) weights; the 1x1 shortcut keeps the [cout][kpad] rows).
 void resblk_split_weights(const float* w, int taps, int cin, int cout, int kpad, uint16_t* hi,
-                          uint16_t* lo, bool frag);
+                          uint16_t* lo, bool frag, float wscale);

@@ -61,8 +61,8 @@ constexpr int TH = 16;                 // output rows per tile (block 1; blocks 
 #endif
 constexpr int TH_NP = RB_TH2;          // output rows per tile of the non-pool blocks 2-3
 constexpr float ACT_SCALE = 16.0f;     // 2^4: every split activation
-constexpr float W_SCALE = 256.0f;      // 2^8: weights (resblk_split_weights)
-constexpr float UNSCALE = 1.0f / (ACT_SCALE * W_SCALE);
+// weights: split at a per-tensor power-of-two scale (resblk_split_weights; the a.u1 / a.u2 / a.us
+// epilogue factors are 2^-4 / that scale)
 constexpr float ACT_RANGE = 65504.0f / ACT_SCALE;
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
@@ -480,7 +480,7 @@ __global__ void __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(R
       const int n = (wn * NTW + nt) * 16 + col;
       const float s2 = ps2[nt];
       const float c2 = fmaf(pb1[nt], s2, pt2[nt]);
-      const f32x2 s2v = {s2 * UNSCALE, s2 * UNSCALE}, c2v = {c2, c2};
+      const f32x2 s2v = {s2 * a.u1, s2 * a.u1}, c2v = {c2, c2};
 #pragma unroll
       for (int m = 0; m < MT1; ++m) {
         const int ih = h0 - 1 + wm * MT1 + m;   // scalar
@@ -597,17 +597,17 @@ __global__ void __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(R
           const int m = 4 * j + 2 * (i >> 1);        // t2 row pair (m, m + 1) of this wave
           const int e = 2 * (i & 1);                  // column pair (e, e + 1) of the lane's 4
           const int oh = h0 + wm * MT2 + m, ow = w0 + 4 * grp + e;   // even
-          float mx = d1[m][nt][e] * UNSCALE;
-          float v01 = d1[m][nt][e + 1] * UNSCALE;
-          float v10 = d1[m + 1][nt][e] * UNSCALE;
-          float v11 = d1[m + 1][nt][e + 1] * UNSCALE;
+          float mx = d1[m][nt][e] * a.u2;
+          float v01 = d1[m][nt][e + 1] * a.u2;
+          float v10 = d1[m + 1][nt][e] * a.u2;
+          float v11 = d1[m + 1][nt][e + 1] * a.u2;
           if (!interior) {   // MaxPool2D 'same' on odd sizes: the window is cut at the edge
             if (oh >= a.h || ow >= a.w) continue;
             if (ow + 1 >= a.w) { v01 = mx; v11 = v10; }
             if (oh + 1 >= a.h) { v10 = mx; v11 = v01; }
           }
           mx = fmaxf(fmaxf(mx, v01), fmaxf(v10, v11));
-          const float sc = e1[j][nt][i] * UNSCALE;
+          const float sc = e1[j][nt][i] * a.us;
           so[(((wm * MT2 + m) >> 1) * PW + ((4 * grp + e) >> 1)) * OPS + n] = mx + sc + b;
         }
     }
@@ -634,7 +634,7 @@ __global__ void __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(R
       for (int m = 0; m < MT2; ++m)
 #pragma unroll
         for (int i = 0; i < 4; ++i)
-          so[((wm * MT2 + m) * TW + 4 * grp + i) * OPS + n] = fmaf(d1[m][nt][i], UNSCALE, b);
+          so[((wm * MT2 + m) * TW + 4 * grp + i) * OPS + n] = fmaf(d1[m][nt][i], a.u2, b);
     }
     __syncthreads();
 #pragma unroll
@@ -699,12 +699,12 @@ static uint16_t f16_bits(float f) {
 }
 
 void resblk_split_weights(const float* w, int taps, int cin, int cout, int kpad, uint16_t* hi,
-                          uint16_t* lo, bool frag) {
+                          uint16_t* lo, bool frag, float wscale) {
   for (size_t i = 0; i < (size_t)cout * kpad; ++i) hi[i] = lo[i] = 0;
   for (int t = 0; t < taps; ++t)
     for (int ci = 0; ci < cin; ++ci)
       for (int co = 0; co < cout; ++co) {
-        const float v = w[((size_t)t * cin + ci) * cout + co] * W_SCALE;   // exact
+        const float v = w[((size_t)t * cin + ci) * cout + co] * wscale;   // exact (power of two)
         const _Float16 h = (_Float16)v;
         const size_t k = (size_t)t * cin + ci;
         // frag: [k / 32][co / 16][lane = co % 16 + 16 (k % 32 / 8)][k % 8] (GEMM 1's B fragments)

@@ -173,21 +173,20 @@ def _segment_index(path):
     return int(os.path.basename(path).split('_')[-3])
 
 
-def post_analysing(root_dir, model, ctx=None, start_time=None, speech=None):
+def post_analysing(root_dir, model, ctx=None, start_time=None, speech_for=None):
     """speaker_identification_post_processing.py:191-312 under ``root_dir`` (the script's
     Root_Dir): speaker labels from the corpus listing, then per directory of
     experiment/recordings/post-time/segments: the stale log removed, the segments sorted by their
     index and each rewritten IN PLACE by the silence removal -- one detector for every segment of
     every conversation, the script's module-level Vad(3) -- 'silent' where fewer than 4000 samples
     survive, the whole standardised conversation's MFCC windows through ONE predict, the TSV log.
-    ``speech`` = list of per-frame decision arrays, one per segment in processing order, replacing
-    the detector (tests).  -> {conversation: labels per window}"""
+    ``speech_for(path)`` -> per-frame decisions for that segment file replaces the detector
+    (tests).  -> {conversation: labels per window}"""
     ctx = ctx or getattr(model, 'ctx', None) or _lib.default_context()
     files = os.listdir(root_dir + '/experiment/corpus/')
     speaker_id_dict = speaker_id_dict_from_corpus(files)
     seg_root = root_dir + '/experiment/recordings/post-time/segments/'
     out = {}
-    k = 0
     for directory_name in os.listdir(seg_root):
         seg_dir = seg_root + directory_name
         whole_wav_path = root_dir + '/experiment/recordings/post-time/standardized/' + directory_name + '.wav'
@@ -201,8 +200,7 @@ def post_analysing(root_dir, model, ctx=None, start_time=None, speech=None):
         silent_index = []
         for segment_no, wav_path in enumerate(paths):
             voiced = remove_silence_file(wav_path, ctx, VAD_OWNER, FRAMERATE, CHANNELS, SAMPWIDTH,
-                                         speech=None if speech is None else speech[k])
-            k += 1
+                                         speech=speech_for(wav_path) if speech_for else None)
             if len(voiced) < SILENT_LEN:
                 silent_index.append(segment_no)
         with wave.open(whole_wav_path, 'rb') as f:
@@ -217,20 +215,20 @@ def post_analysing(root_dir, model, ctx=None, start_time=None, speech=None):
     return out
 
 
-def run_offline(root_dir, model, noise_path=None, ctx=None, start_time=None, speech=None):
+def run_offline(root_dir, model, noise_path=None, ctx=None, start_time=None, speech_for=None):
     """The script's ``__main__`` (:315-353) without the transfer learning (training is out of
     scope: ``model`` is the already trained experiment model): standardise every corpus file in
     place (dbfs=0, silence removal), standardise the conversations of post-time/whole (zoom*: no
     noise gate, audio*: three passes), cut them into 2.56 s segments, post_analysing.
-    ``speech`` = per-frame decisions for every silence-removal call in order (tests)."""
+    ``speech_for(path)`` -> per-frame decisions for a file's silence removal replaces the detector
+    (tests)."""
     ctx = ctx or getattr(model, 'ctx', None) or _lib.default_context()
     noise_path = noise_path or os.path.join(root_dir, 'experiment/Ambient_Noise.wav')
-    it = iter(speech) if speech is not None else None
-    nxt = (lambda: next(it)) if it is not None else (lambda: None)
     for (dirpath, dirnames, filenames) in os.walk(root_dir + '/experiment/corpus/'):
         for filename in filenames:
-            standardize_audio(os.sep.join([dirpath, filename]), dbfs=0, noise_reduced=0,
-                              silence_remove=True, noise_path=noise_path, ctx=ctx, speech=nxt())
+            path = os.sep.join([dirpath, filename])
+            standardize_audio(path, dbfs=0, noise_reduced=0, silence_remove=True, noise_path=noise_path,
+                              ctx=ctx, speech=speech_for(path) if speech_for else None)
     whole = root_dir + '/experiment/recordings/post-time/whole/'
     for audio_file_name in os.listdir(whole):
         src = os.path.join(whole, audio_file_name)
@@ -242,5 +240,4 @@ def run_offline(root_dir, model, noise_path=None, ctx=None, start_time=None, spe
             standardize_audio(src, dst, dbfs=0, noise_reduced=3, noise_path=noise_path, ctx=ctx)
     segmentation_si(root_dir + '/experiment/recordings/post-time/standardized/',
                     root_dir + '/experiment/recordings/post-time/segments/', 2.56, 2.56)
-    rest = list(it) if it is not None else None
-    return post_analysing(root_dir, model, ctx, start_time, rest)
+    return post_analysing(root_dir, model, ctx, start_time, speech_for)

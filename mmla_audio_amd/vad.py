@@ -30,7 +30,12 @@ class Frame:
 
 def frame_generator(frame_duration_ms, audio, sample_rate):
     """record_on_pc.py:229-243: frames of `frame_duration_ms` from PCM bytes, the last partial (or
-    exactly final) frame dropped"""
+    exactly final) frame dropped.
+
+    Origin: the reference's function is py-webrtcvad's example.py ``frame_generator`` (MIT licence,
+    John Wiseman), which the reference copied.  These lines restate it on purpose: the frame
+    boundaries (and the strict ``<`` that drops an exactly final frame) decide which samples the VAD
+    collector keeps, so the drop-in must frame exactly as the reference does."""
     n = int(sample_rate * (frame_duration_ms / 1000.0) * 2)
     offset = 0
     timestamp = 0.0

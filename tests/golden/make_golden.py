@@ -532,12 +532,14 @@ def _odpost_case(ofg_mod, tmp):
             x = np.clip(np.round(np.stack(ch, axis=1)), -32768, 32767).astype(np.int16)
             wavfile.write(os.path.join(pt, 'whole', name), 48000, x)
             out[f'pcm_{i}'] = x
+            out[f'rate_{i}'] = np.array(48000)
             continue
         pieces = [synth.clip(sd, 40000).astype(np.float64) * 0.5 for sd in seeds]
         x = np.concatenate(pieces)[:n] + rng.standard_normal(n) * 300
         x = np.clip(np.round(x), -32768, 32767).astype(np.int16)
         _write_wav(os.path.join(pt, 'whole', name), x)
         out[f'pcm_{i}'] = x
+        out[f'rate_{i}'] = np.array(16000)
 
     class FixedClock(_dt.datetime):
         @classmethod

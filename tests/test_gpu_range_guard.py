@@ -2,8 +2,8 @@
 
 The default arithmetic splits every conv / LSTM operand into fp16 hi + lo; a value >= 65504 would
 become inf and could be masked downstream (ELU(-inf) = -1, MaxPool, LSTM saturation) into a finite,
-wrong class.  Weights outside the range make the model run exact f32 at load time; activations
-outside it are flagged by the kernel that splits them: host-pointer calls re-run the micro-batch in
+wrong class.  Weights are split at a per-tensor power-of-two scale (any finite tensor fits; a
+non-finite one makes the model run exact f32 at load time); activations outside the range are flagged by the kernel that splits them: host-pointer calls re-run the micro-batch in
 exact f32 (bit-identical to MMLA_PREC_F32), device-pointer calls report MMLA_E_RANGE.
 """
 import numpy as np
@@ -69,20 +69,58 @@ def test_od_activation_overflow_device_call_reports_range():
     assert c.range_check() == 0                   # reported once, then cleared
 
 
-@pytest.mark.parametrize('big', [300.0, 7.0e4])
-def test_out_of_range_weights_run_exact_f32(big):
-    """conv_h3 splits w * 2^8: |w| >= 65504 / 2^8 (= 255.9) already leaves the fp16 range"""
+def test_nonfinite_weights_run_exact_f32():
+    """a weight tensor holding inf / NaN cannot be split: that model runs exact f32 (load time)"""
     from mmla_audio_amd import _lib, weights
     W = weights.synthetic(weights.OD, seed=6)
     W['layer_with_weights-20/kernel'] = W['layer_with_weights-20/kernel'].copy()
-    W['layer_with_weights-20/kernel'][0, 0, 0, 0] = big      # block 5's 3x3 conv
+    W['layer_with_weights-20/kernel'][0, 0, 0, 0] = np.inf      # block 5's 3x3 conv
     pcm = synth.batch(330, 6, 40000)
     c = _ctx(W_od=W)
     p, a, _ = c.od_pipeline(pcm)
     ref = _ctx(W_od=W, prec=_lib.PREC_F32)
     p32, a32, _ = ref.od_pipeline(pcm)
-    assert np.array_equal(p, p32) and np.array_equal(a, a32)
+    assert np.array_equal(p, p32, equal_nan=True) and np.array_equal(a, a32)
     assert c.range_check() == 0                   # decided at load time, nothing re-run
+
+
+def _scaled_od(f, seed=16):
+    """OD weights with every 3x3 conv kernel and bias x f (its BatchNorm's moving mean x f and
+    variance x f^2, so the block still sees O(1) activations) and the BiLSTM kernels x f"""
+    from mmla_audio_amd import weights
+    W = weights.synthetic(weights.OD, seed=seed)
+    names = [e[0] for e in weights.spec(weights.OD)]
+    for i, name in enumerate(names):
+        if name.endswith('/kernel') and W[name].ndim == 4 and W[name].shape[:2] == (3, 3):
+            W[name] = W[name] * f
+            W[name.replace('/kernel', '/bias')] = W[name.replace('/kernel', '/bias')] * f
+            bn = next(m for m in names[i:] if m.endswith('/moving_variance'))
+            W[bn] = W[bn] * f * f
+            W[bn.replace('moving_variance', 'moving_mean')] = W[bn.replace('moving_variance', 'moving_mean')] * f
+        if 'layer_with_weights-40/' in name and name.endswith('kernel'):
+            W[name] = W[name] * f
+    return W
+
+
+@pytest.mark.parametrize('f', [1.0e4, 1.0e-3])
+def test_scaled_weights_stay_on_3xfp16(f):
+    """each weight tensor is split at its own power-of-two scale, so weights far
+    outside the old fixed 2^8 window (|w| up to ~1.5e3 here, or ~1e-4) keep the 3xFP16 path:
+    log-probabilities within 1e-4 of the float64 oracle, nothing flagged, no exact-f32 fallback"""
+    from mmla_audio_amd import _lib
+    from oracle import compare, nets
+    W = _scaled_od(f)
+    m = [float(np.abs(W[k]).max()) for k in W if k.endswith('kernel')]
+    assert max(m) > 255.9 if f > 1 else min(m) < 1e-3        # outside the old fixed 2^8 window
+    x = np.random.default_rng(17).integers(0, 256, size=(6, 128, 151, 3)).astype(np.uint8)
+    c = _ctx(W_od=W)
+    p = c.od_forward(x)
+    assert c.range_check() == 0
+    ref = nets.od_forward(x.astype(np.float32), W)
+    assert compare.logp_err(p, ref) <= compare.LOGP_TOL, compare.logp_err(p, ref)
+    assert compare.argmax_ok(p, ref)
+    p32 = _ctx(W_od=W, prec=_lib.PREC_F32).od_forward(x)
+    assert not np.array_equal(p, p32)             # really the 3xFP16 arithmetic, not the f32 path
 
 
 def test_si_lstm_input_overflow_host_call_reruns_in_f32():
