@@ -349,6 +349,17 @@ __global__ void __launch_bounds__(NT, (conv_minw<KH, BN, TW, EPI, SHP::FIXED>())
       if (task >= nstg * QPP) continue;
       const int px = task / QPP, q = task % QPP;
       float4 v = pre[j];
+#if CONV_H3_RAWSTAGE
+      // dev timing build: the staging of a producer-split input (the 4 bytes of each element already
+      // hold its fp16 hi / lo) -- no prologue, range check or split
+      {
+        const uint2 u0 = {__builtin_bit_cast(uint32_t, v.x), __builtin_bit_cast(uint32_t, v.y)};
+        const uint2 u1 = {__builtin_bit_cast(uint32_t, v.z), __builtin_bit_cast(uint32_t, v.w)};
+        *reinterpret_cast<uint2*>(lds_hi + px * LDP + q * 4) = u0;
+        *reinterpret_cast<uint2*>(lds_lo + px * LDP + q * 4) = u1;
+        continue;
+      }
+#endif
       if constexpr (PRO != PRO_NONE) {
         if (valid & (1u << j)) {
           const float4 sc = psc, sh = psh;

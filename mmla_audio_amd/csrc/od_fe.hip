@@ -732,6 +732,15 @@ MMLA_DEV uint32_t split1(float x) {   // x: a plain VALU result (staging), no MF
       : "=&v"(u) : "v"(x));
   return u;
 }
+// x' = x s with s a power of two in an SGPR (the staging's 2^-12), both halves by v_fma_mix: the
+// scaling rides on the conversions (x s exact, rounded once to the hi half; x s - hi exact in f16)
+MMLA_DEV uint32_t split1s(float x, float s) {
+  uint32_t u;
+  asm("v_fma_mixlo_f16 %0, %1, %2, 0\n\t"
+      "v_fma_mixhi_f16 %0, %1, %2, -%0 op_sel_hi:[0,0,1]"
+      : "=&v"(u) : "v"(x), "s"(s));
+  return u;
+}
 // two values: hi = (f16(a), f16(b)), lo = (f16(a - hi.a), f16(b - hi.b))
 MMLA_DEV void split2(float a, float b, uint32_t& hi, uint32_t& lo) {
   hi = __builtin_bit_cast(uint32_t, __builtin_convertvector((f2v){a, b}, h2));
@@ -760,11 +769,10 @@ MMLA_DEV int s2_bin(int k2, int i) {
   return i < 8 ? 25 * i + k2 : 25 * (i - 8) + 25 - k2;
 }
 
-// 10 log10 max(s, 1e-10) as db10, the clamp as one med3 (fmaxf would add a NaN-quieting max;
-// mel sums are never NaN)
-MMLA_DEV float db10m(float s) {
-  return __log2f(__builtin_amdgcn_fmed3f(s, 1e-10f, __builtin_inff())) * 3.0102999566398120f;
-}
+// log2 max(s, 1e-10) (the mel keeps this; the epilogue's fma applies 10 log10 2), the clamp as one
+// med3 (fmaxf would add a NaN-quieting max; mel sums are never NaN)
+MMLA_DEV float lg2m(float s) { return __log2f(__builtin_amdgcn_fmed3f(s, 1e-10f, __builtin_inff())); }
+constexpr float DB_PER_LOG2 = 3.0102999566398120f;
 
 // wave-wide max / min through DPP (quad_perm, row_ror) and four readlanes: no lane-index registers
 template <bool MAX>
@@ -882,6 +890,9 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
   auto clip_in = [&](int64_t clip) -> ClipIn {
     ClipIn ci;
     int len = a.lens ? a.lens[clip] : a.clip_len;
+    // wave-uniform in an SGPR: the prefetch's buffer descriptor (num_records = 2 len) then needs no
+    // waterfall loop over lanes
+    len = __builtin_amdgcn_readfirstlane(len);
     ci.len = len < 0 ? 0 : (len > CLIP ? CLIP : len);
     ci.src = a.pcm + clip * a.clip_stride;
     ci.fast = !a.pcm_f32 && (reinterpret_cast<uintptr_t>(ci.src) & 15) == 0;
@@ -991,14 +1002,15 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
       }
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        d[2 * k] = split1((float)(int16_t)(w[k] & 0xffffu) * X_SCALE);
-        d[2 * k + 1] = split1((float)(int16_t)(w[k] >> 16) * X_SCALE);
+        d[2 * k] = split1s((float)(int16_t)(w[k] & 0xffffu), X_SCALE);
+        d[2 * k + 1] = split1s((float)(int16_t)(w[k] >> 16), X_SCALE);
       }
-      // sign bits: the high byte of each sample gathered (perm), bit 7 of each byte packed
-      const uint32_t h01 = __builtin_amdgcn_perm(w[1], w[0], 0x07050301u);
-      const uint32_t h23 = __builtin_amdgcn_perm(w[3], w[2], 0x07050301u);
-      sg = ((((h01 >> 7) & 0x01010101u) * 0x01020408u) >> 24) |
-           (((((h23 >> 7) & 0x01010101u) * 0x01020408u) >> 24) << 4);
+      // sign bits: v_perm's selectors 8..11 give 0xff / 0x00 from the sign of bytes 1, 3, 5, 7 (the
+      // samples' high bytes); a signed dot4 with weights -1, -2, -4, ... packs them (4 full-rate ops)
+      const int s01 = (int)__builtin_amdgcn_perm(w[1], w[0], 0x0b0a0908u);
+      const int s23 = (int)__builtin_amdgcn_perm(w[3], w[2], 0x0b0a0908u);
+      sg = (uint32_t)__builtin_amdgcn_sdot4(s23, (int)0x80c0e0f0u,
+                                            __builtin_amdgcn_sdot4(s01, (int)0xf8fcfeffu, 0, false), false);
     }
     if (live) {
       uint32_t* tq = sm.t + (c & 1) * 8 * TP + (c >> 1);
@@ -1121,18 +1133,26 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
       // 25 (i - 8) + 25 - k2; GEMM 0 has bins 25 i for i <= 8 only (the other lanes write the
       // trash row).  Branch-free: the row offset is an immediate plus the wave-uniform k2
       float* prow = P + 50 * PP * hh + r;
-      float* trash = P + PTRASH * PP + lane;
+      // one scalar branch per GEMM (not per pair): the k2 = 0 GEMM's row pattern apart, so the other
+      // twelve waves store each power with one immediate-offset write from two base registers
+      if (k2 == 0) {
+        float* trash = P + PTRASH * PP + lane;
 #pragma unroll
-      for (int pi = 0; pi < 8; ++pi) {
-        const int c0 = (pi & 1) + 4 * (pi >> 1);
-        const float re = acc[2 * pi], im = acc[2 * pi + 1];
-        const float pw = fmaf(re, re, im * im);
-        if (k2 == 0) {
-          if (c0 <= 8) *(c0 + 2 * hh <= 8 ? prow + 25 * c0 * PP : trash) = pw;
-        } else if (c0 < 8) {
-          prow[(25 * c0 + k2) * PP] = pw;
-        } else {
-          prow[(25 * (c0 - 8) + 25 - k2) * PP] = pw;
+        for (int pi = 0; pi < 8; ++pi) {
+          const int c0 = (pi & 1) + 4 * (pi >> 1);
+          if (c0 > 8) continue;
+          const float pw = fmaf(acc[2 * pi], acc[2 * pi], acc[2 * pi + 1] * acc[2 * pi + 1]);
+          *(c0 + 2 * hh <= 8 ? prow + 25 * c0 * PP : trash) = pw;
+        }
+      } else {
+        float* const pa = prow + k2 * PP;            // bins 25 c0 + k2       (c0 < 8)
+        float* const pb = prow + (25 - k2) * PP;     // bins 25 (c0 - 8) + 25 - k2
+#pragma unroll
+        for (int pi = 0; pi < 8; ++pi) {
+          const int c0 = (pi & 1) + 4 * (pi >> 1);
+          const float pw = fmaf(acc[2 * pi], acc[2 * pi], acc[2 * pi + 1] * acc[2 * pi + 1]);
+          if (c0 < 8) pa[25 * c0 * PP] = pw;
+          else pb[25 * (c0 - 8) * PP] = pw;
         }
       }
     }
@@ -1149,7 +1169,7 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
 #pragma unroll
       for (int k = 0; k < 13; ++k) {
         const uint32_t w = cw[k] & (k == 12 ? 0x0f0fu : 0x0f0f0f0fu);
-        s += (int)((w * 0x01010101u) >> 24);
+        s = (int)__builtin_amdgcn_udot4(w, 0x01010101u, (uint32_t)s, false);   // the 4 byte counts
       }
       s -= (int)((cw[0] >> 4) & 1u);
       if (TF * t + lane < NF) sm.zc[par][TF * t + lane] = s;
@@ -1162,7 +1182,7 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
   const int m_bin0 = __builtin_amdgcn_readfirstlane(tb.mel_bt_bin0[m_bt]);
   const int m_nk = __builtin_amdgcn_readfirstlane(tb.mel_bt_nk[m_bt]);
   const int m_frag = __builtin_amdgcn_readfirstlane(tb.mel_bt_frag[m_bt]);
-  // 10 log10 S at band 16 bt + 4 (l >> 4) + i, frame 32 t + 16 fh + (l & 15)
+  // log2 S at band 16 bt + 4 (l >> 4) + i, frame 32 t + 16 fh + (l & 15)
   float dbv[NTILE][4];
   float smax = 0.0f, smin = INFINITY;
   typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -1198,7 +1218,7 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
     const bool live = TF * t + TF <= NF || TF * t + 16 * m_fh + (l & 15) < NF;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      dbv[t][i] = db10m(acc[i]);
+      dbv[t][i] = lg2m(acc[i]);
       if (live) {
         smax = fmaxf(smax, acc[i]);
         smin = fminf(smin, acc[i]);
@@ -1217,13 +1237,16 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
       mx = fmaxf(mx, sm.red[0][w]);
       mn = fminf(mn, sm.red[1][w]);
     }
-    // ref = np.max: numpy takes 10 log10 of the float32 max in float64 and subtracts it in float32;
-    // the kernel's own db10 of the max is within an ulp of that and makes d_max exactly 0 (the shift
-    // cancels in the normalisation; the dB outputs move by ~1e-5 dB, tolerance 5e-3)
-    const float ref_db = db10m(mx);
-    const float d_max = db10m(mx) - ref_db;
+    // ref = np.max: numpy takes 10 log10 of the float32 max in float64 and subtracts it in float32.
+    // Here every dB value is fma(log2 S, 10 log10 2, -ref) with ref = the rounded dB of the max, the
+    // max and min taken through the same expression: d_max is within an ulp of 0 (the shift cancels
+    // in the normalisation; the dB outputs move by ~1e-5 dB, tolerance 5e-3), the clip's min maps to
+    // exactly 0, a constant spectrum (digital silence) to 0 / 0 = NaN as the reference
+    const float lmx = lg2m(mx);
+    const float nref = -(lmx * DB_PER_LOG2);
+    const float d_max = fmaf(lmx, DB_PER_LOG2, nref);
     const float thr = d_max - 80.0f;
-    const float d_min = fmaxf(db10m(mn) - ref_db, thr);
+    const float d_min = fmaxf(fmaf(lg2m(mn), DB_PER_LOG2, nref), thr);
     const float diff = d_max - d_min;
     const float inv_diff = 1.0f / diff;
     const int tz = otid();
@@ -1252,20 +1275,21 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
       if (IMG) rr = (uint32_t)(int)(((double)sm.zc[par][TF * t + fr] / 400.0) * 255.0) & 255u;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const float d = fmaxf(dbv[t][i] - ref_db, thr);
+        const float d = fmaxf(fmaf(dbv[t][i], DB_PER_LOG2, nref), thr);
         // (d - min) / (max - min) as a multiply by the reciprocal (<= 2 ulp; as v2); 0 * inf =
-        // NaN keeps the digital-silence NaN
+        // NaN keeps the digital-silence NaN.  The (i, t) part of the offset is wave-uniform: it
+        // rides in soffset (a scalar add), the lane's part is the one VGPR vf
         const float nv = (d - d_min) * inv_diff;
-        const uint32_t of = vf + (uint32_t)(i * NF + TF * t) * 4u;
-        if (NM && !(FE3_SKIP & 16)) __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, nv), rn, of, sf, 0);
-        if (DB) __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, d), rd, of, sf, 0);
+        const int so = sf + (i * NF + TF * t) * 4;
+        if (NM && !(FE3_SKIP & 16)) __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, nv), rn, vf, so, 0);
+        if (DB) __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, d), rd, vf, so, 0);
         if (IMG) {
           const double v = (1.0 - (double)nv) * 255.0;
           const uint32_t gb = (v >= 0.0) ? ((uint32_t)(int)v & 255u) : 0u;
-          const uint32_t oi = vi + (uint32_t)((3 - i) * NF + TF * t) * 3u;
-          __builtin_amdgcn_raw_buffer_store_b8((uint8_t)rr, ri, oi, si, 0);
-          __builtin_amdgcn_raw_buffer_store_b8((uint8_t)gb, ri, oi + 1, si, 0);
-          __builtin_amdgcn_raw_buffer_store_b8((uint8_t)gb, ri, oi + 2, si, 0);
+          const int soi = si + ((3 - i) * NF + TF * t) * 3;
+          __builtin_amdgcn_raw_buffer_store_b8((uint8_t)rr, ri, vi, soi, 0);
+          __builtin_amdgcn_raw_buffer_store_b8((uint8_t)gb, ri, vi + 1, soi, 0);
+          __builtin_amdgcn_raw_buffer_store_b8((uint8_t)gb, ri, vi + 2, soi, 0);
         }
       }
     }
