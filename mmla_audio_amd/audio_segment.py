@@ -18,6 +18,7 @@ GPU (mmla_ratecv, resample.hip; bit-identical to CPython's audioop, tests/test_g
 resampy's sinc interpolation on the GPU (mmla_resample_sinc) with the ``kaiser_best`` filter built
 here -- resampy is not installed in this image, so that step's parity is unpinned.
 """
+import math
 import wave
 
 import numpy as np
@@ -160,11 +161,13 @@ class AudioSegment:
 
     @property
     def dBFS(self):
-        """pydub: ratio_to_db(rms / max_possible_amplitude); -inf for silence"""
+        """pydub: ratio_to_db(rms / max_possible_amplitude) = 20 * math.log(ratio, 10) (pydub's own
+        expression: math.log with a base is log(x) / log(10), which can differ from log10 in the
+        last bit); -inf for silence"""
         rms = self.rms
         if not rms:
             return -float('inf')
-        return 20.0 * np.log10(rms / float(self.max_possible_amplitude))
+        return 20 * math.log(rms / float(self.max_possible_amplitude), 10)
 
     def apply_gain(self, volume_change):
         """audioop.mul(data, 2, 10 ** (volume_change / 20)): per sample x * factor in double,

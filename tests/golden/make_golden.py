@@ -46,6 +46,7 @@ Output: tests/golden/{od,si,seg,si_experiment,vad,sipost}_golden.npz (small, com
 """
 import hashlib
 import io
+import math
 import os
 import sys
 import tempfile
@@ -153,7 +154,7 @@ class AudioopSegment:
     def dBFS(self):
         import audioop
         rms = audioop.rms(self._data, 2)
-        return 20 * np.log10(rms / 32768.0) if rms else -float('inf')
+        return 20 * math.log(rms / 32768.0, 10) if rms else -float('inf')   # pydub ratio_to_db
 
     def apply_gain(self, volume_change):
         import audioop

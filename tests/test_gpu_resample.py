@@ -5,6 +5,7 @@ overlap_detection_post_processing.py:120-121, speaker_identification_post_proces
 bit-identical.  mmla_resample_sinc against the oracle's resampy restatement with the same filter
 table: bit-identical (resampy itself is absent: parity with the library unpinned).
 """
+import math
 import warnings
 
 import numpy as np
@@ -61,3 +62,29 @@ def test_resample_sinc_matches_restatement(ctx, sr0, sr1):
         assert np.array_equal(got, want), (sr0, sr1, n, np.abs(got - want).max())
     y = resample(x, sr0, sr1, ctx)                      # + librosa's fix_length
     assert np.array_equal(y, ors.librosa_resample(x, sr0, sr1, table))
+
+
+@pytest.mark.parametrize('dbfs', [-20, -3.5])
+def test_od_standardize_audio_gain(ctx, tmp_path, dbfs):
+    """OD standardize_audio(source, target, format, dbfs) with a gain target (the reference's
+    post_anlysing passes dbfs=0, which skips it): pydub set_frame_rate -> apply_gain(dbfs - dBFS)
+    -> export, i.e. audioop.ratecv -> audioop.rms -> audioop.mul, byte for byte
+    (overlap_detection_post_processing.py:101-125)"""
+    import wave
+    from mmla_audio_amd.overlap_detection_post_processing import standardize_audio
+    rng = np.random.default_rng(11)
+    x = (rng.standard_normal(2 * 44100) * 3000).clip(-32768, 32767).astype('<i2')   # 1 s stereo
+    src, dst = str(tmp_path / 'zoom_a.wav'), str(tmp_path / 'zoom_a_std.wav')
+    with wave.open(src, 'wb') as f:
+        f.setnchannels(2)
+        f.setsampwidth(2)
+        f.setframerate(44100)
+        f.writeframes(x.tobytes())
+    pcm = standardize_audio(src, dst, None, dbfs, ctx=ctx)
+    conv = audioop.ratecv(x.tobytes(), 2, 2, 44100, 16000, None)[0]
+    level = 20 * math.log(audioop.rms(conv, 2) / 32768.0, 10)   # pydub ratio_to_db
+    want = np.frombuffer(audioop.mul(conv, 2, 10 ** ((dbfs - level) / 20)), '<i2')
+    assert np.array_equal(pcm, want)
+    with wave.open(dst, 'rb') as f:
+        assert (f.getnchannels(), f.getframerate()) == (2, 16000)
+        assert np.array_equal(np.frombuffer(f.readframes(f.getnframes()), '<i2'), want)

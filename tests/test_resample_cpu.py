@@ -6,6 +6,7 @@ SpeakerIdentification/scripts/speaker_identification_post_processing.py:159-164)
 this image's Python 3.10, so the oracle's closed-form ratecv (which the GPU kernel implements) and the
 drop-in's host mul / rms are checked against the real thing here.
 """
+import math
 import warnings
 
 import numpy as np
@@ -50,8 +51,8 @@ def test_mul_and_rms_match_audioop():
         seg = AudioSegment(pcm, 16000)
         assert seg.rms == audioop.rms(pcm.astype('<i2').tobytes(), 2)
     seg = AudioSegment(x, 16000)
-    # pydub: dBFS = 20 log10(rms / 2^15); apply_gain(d) = mul by 10^(d/20)
-    assert seg.dBFS == pytest.approx(20 * np.log10(audioop.rms(x.tobytes(), 2) / 32768.0), abs=0)
+    # pydub: dBFS = 20 math.log(rms / 2^15, 10); apply_gain(d) = mul by 10^(d/20)
+    assert seg.dBFS == 20 * math.log(audioop.rms(x.tobytes(), 2) / 32768.0, 10)   # pydub ratio_to_db
     g = seg.apply_gain(-20 - seg.dBFS)
     want = np.frombuffer(audioop.mul(x.tobytes(), 2, 10 ** ((-20 - seg.dBFS) / 20)), '<i2')
     assert np.array_equal(g.data, want)
