@@ -59,6 +59,18 @@ def test_od_features_ragged_lengths(ctx):
                  for i, p in enumerate(pcm)])
 
 
+def test_si_features_worst_case_tones(ctx):
+    """tests/test_si_precision.py: near-Nyquist full-scale tones, where a float32 FFT misses the 1e-4
+    bar (2.4e-4 at 7980 Hz); the float64 kernel stays far inside it"""
+    t = np.arange(24000) / 16000.0
+    clips = [np.round(32767 * np.sin(2 * np.pi * f * t)).astype(np.int16) for f in (7950, 7980, 7900, 7999, 100)]
+    feat, silent = ctx.si_features(clips)
+    for i, p in enumerate(clips):
+        want = si_fe.input_feature_gen(p)[0]
+        err = np.abs(feat[i] - want).max()
+        assert not silent[i] and err <= 1e-5, f'clip {i}: SI err {err}'
+
+
 def test_si_features_golden(ctx, si_golden):
     names = list(si_golden['names'])
     pcms = [si_golden[f'pcm_{i}'] for i in range(len(names))]
