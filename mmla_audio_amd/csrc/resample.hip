@@ -47,7 +47,10 @@ __global__ void sinc_resample_kernel(SincResampleArgs a) {
   if (t >= a.n_out) return;
   const double2* __restrict__ wd = reinterpret_cast<const double2*>(a.win);   // (win, dwin) pairs
   const double tr = a.tr[t];
-  const int64_t n = (int64_t)tr;
+  // n <= n_orig - 1 for every rate pair (the last time is ~ n_orig - 1 / ratio); clamped anyway so a
+  // time register that drifted past the input (ratios far beyond audio's) cannot read past x
+  int64_t n = (int64_t)tr;
+  n = n < a.n_orig ? n : a.n_orig - 1;
   double frac = a.scale * (tr - (double)n);
   double index_frac = frac * (double)a.num_table;
   int64_t offset = (int64_t)index_frac;
