@@ -12,7 +12,7 @@ speaker_identification_post_processing.py:136-188) goes through
 ``AudioSegment`` keeps pydub's semantics for 16-bit WAV data of any channel count and rate:
 ``set_frame_rate`` is ``audioop.ratecv(data, 2, channels, rate, new_rate, None)`` and runs on the
 GPU (mmla_ratecv, resample.hip; bit-identical to CPython's audioop, tests/test_gpu_resample.py);
-``dBFS`` is ``20 log10(audioop.rms / 2^15)`` and ``apply_gain`` ``audioop.mul(data, 2,
+``dBFS`` is pydub's ``20 * math.log(audioop.rms / 2^15, 10)`` and ``apply_gain`` ``audioop.mul(data, 2,
 10^(db/20))`` (host arithmetic, pinned against stdlib audioop in tests/test_resample_cpu.py).
 ``load`` is librosa.load(path, sr=22050 | None, mono=True) for WAV files; its resampling step is
 resampy's sinc interpolation on the GPU (mmla_resample_sinc) with the ``kaiser_best`` filter built

@@ -139,7 +139,7 @@ def _write_pcm16(path, pcm, rate=16000, channels=1):
 
 
 def pcm_dbfs(pcm):
-    """pydub ``AudioSegment.dBFS`` of 16-bit audio: 20 log10(audioop.rms / 2^15), audioop.rms being
+    """pydub ``AudioSegment.dBFS`` of 16-bit audio: 20 math.log(audioop.rms / 2^15, 10), audioop.rms being
     the integer part of sqrt(mean(x^2)); -inf for silence."""
     return AudioSegment(pcm, 16000).dBFS
 
