@@ -4,7 +4,7 @@
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-for v in 0 1 2 4 8 16; do
+for v in ${SKIPS:-0 1 2 4 8 16}; do
   if [ $v = 0 ]; then lib=mmla_audio_amd/libmmla.so; else lib=mmla_audio_amd/ab/libmmla_skip$v.so; fi
   rm -rf gpurun_out/fpmc_$v
   timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_MFMA SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES --output-format csv -d gpurun_out/fpmc_$v -o p -- python3 tools/bench_with_lib.py $lib --workload od_features --clips 4096 --steps 1 --warmup 0 --no-cpu-baseline --no-f32 --no-parity --no-latency > gpurun_out/fpmc_$v.log 2>&1 || { echo "pass $v failed"; tail -5 gpurun_out/fpmc_$v.log; exit 1; }
