@@ -209,7 +209,7 @@ struct Smem {
   uint8_t rb[NF + 1];              // image R byte per column
   float red[2][NW];                // per-wave max / min of the mel power
 };
-constexpr int64_t NW4_MAX_CLIPS = 8192;   // launches up to this size use four waves per clip
+[[maybe_unused]] constexpr int64_t NW4_MAX_CLIPS = 8192;   // (A/B builds) launches up to this size use four waves per clip
 static_assert(sizeof(int16_t) * WIN % 16 == 0, "st must stay 16-B aligned");
 static_assert(sizeof(WaveBuf) % 16 == 0, "wave buffers stay 16-B aligned");
 static_assert(P2W * sizeof(float2) <= 2 * 200 * sizeof(cf), "a pair's power row fits its FFT rows");
