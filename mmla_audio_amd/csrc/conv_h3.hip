@@ -74,7 +74,15 @@ MMLA_DEV float pro_fn(float v, float sc, float sh) {
 // at occupancy 2; the 3x3 TW 16 variant is slower with them (3.31 -> 3.54) and keeps 128.  BN 128
 // halved to 64 pixels (occupancy 4) was 25-33 % slower: per-tile costs dominate, not latency.
 template <int KH, int BN, int TW>
-constexpr int tile_px() { return BN == 64 && TW > 1 && !(KH == 3 && TW == 16) ? 256 : BM; }
+// the SI Conv1D layers with BN <= 64 (K = 3 x 32 or 3 x 64: little work per row) take 256-row tiles:
+// the per-tile fixed costs (B fragments, bias, setup) over twice the rows -- SI conv 41.05 -> 40.51 ms
+// per 3 steps, outputs bit-identical (A/B, round 4)
+#ifndef CONV_SI_ROWS
+#define CONV_SI_ROWS 256
+#endif
+constexpr int tile_px() {
+  return BN == 64 && TW > 1 && !(KH == 3 && TW == 16) ? 256 : (TW == 1 && BN <= 64 ? CONV_SI_ROWS : BM);
+}
 
 // TW == 0 (LIN): a tile is 128 consecutive pixels of the whole batch in NHWC order (rows of all
 // clips back to back), so the 19-wide images do not pad 19 -> 24 columns.  The rows the tile touches
