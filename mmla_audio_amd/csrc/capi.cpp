@@ -23,6 +23,7 @@
 #include "nr.h"
 #include "vad.h"
 #include "resample.h"
+#include "siu.h"
 
 namespace {
 
@@ -125,6 +126,9 @@ struct mmla_ctx {
   int64_t od_mb_cap = kOdMicrobatch, si_mb_cap = kSiMicrobatch;   // default caps of the automatic size
   int debug_fail_allocs = 0;   // test hook (env MMLA_DEBUG_FAIL_ALLOC at create): fail this many workspace allocations
   int precision = MMLA_PREC_F16X3;
+  // SI res units without pooling as one fused kernel each (siu.hip); env MMLA_NO_SIU=1 at create:
+  // the two conv_h3 launches (A/B)
+  bool siu = true;
   // 3xFP16 range guard: kernels set range_dev[0] (device-pointer calls; sticky until
   // mmla_range_check) or range_dev[1] (host-pointer micro-batches: re-run in exact f32) when an
   // operand they split into fp16 is >= 65504 in magnitude or not finite
@@ -917,6 +921,30 @@ int run_si_net(mmla_ctx* c, const float* x, int64_t n, float* probs, int32_t* ar
       }
       std::swap(X, R);
       t = tp;
+    } else if (c->siu && c->precision == MMLA_PREC_F16X3 && U.ca.wh && U.cb.wh && siu_supported(cin) &&
+               U.ca.cout == cin && U.cb.cin == cin && U.cb.cout == cin && U.ca.cin_pad == cin &&
+               U.ca.cout_pad == cin && U.cb.cout_pad == cin) {
+      // the whole unit in one launch, t1 kept on chip (siu.hip), bit-identical to the pair below
+      SiuArgs s{};
+      s.x = X;
+      s.y = R;
+      s.wah = U.ca.wh;
+      s.wal = U.ca.wl;
+      s.wbh = U.cb.wh;
+      s.wbl = U.cb.wl;
+      s.ba = U.ca.bias;
+      s.bb = U.cb.bias;
+      s.s_in = U.bn_in.scale;
+      s.t_in = U.bn_in.shift;
+      s.s_mid = U.bn_mid.scale;
+      s.t_mid = U.bn_mid.shift;
+      s.ua = U.ca.unscale();
+      s.ub = U.cb.unscale();
+      s.n = (int)n;
+      s.t = t;
+      s.range_flag = c->range_ptr;
+      LAUNCH(c, MMLA_STAGE_CONV, 2.0 * 2.0 * n * t * 3 * cin * cin, siu_launch(s, cin, c->stream));
+      std::swap(X, R);
     } else {
       CHK(conv_spatial(c, U.ca, X, T1, (int)n, t, 1, &U.bn_in, PRO_BN_RELU, EPI_BIAS, nullptr));
       CHK(conv_spatial(c, U.cb, T1, X, (int)n, t, 1, &U.bn_mid, PRO_BN_RELU, EPI_ADD, X));
@@ -1000,6 +1028,7 @@ int mmla_create(int device, mmla_ctx** out) {
   mmla_ctx* c = new mmla_ctx();
   c->device = device;
   if (const char* fa = std::getenv("MMLA_DEBUG_FAIL_ALLOC")) c->debug_fail_allocs = std::atoi(fa);
+  if (const char* su = std::getenv("MMLA_NO_SIU")) c->siu = std::atoi(su) == 0;
   // a BLOCKING stream: it orders with the legacy default (NULL) stream, on which PyTorch's default
   // stream enqueues -- so a device-pointer call sees tensors a torch kernel or copy just produced
   // without an explicit synchronisation (a non-blocking stream raced them: a 65 536-clip call read

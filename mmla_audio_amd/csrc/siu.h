@@ -1,0 +1,25 @@
+// One SpeakerIdentification res_unit without pooling as a single fused kernel.  See siu.hip.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+struct SiuArgs {
+  const float* x;          // [n * t, C] the unit's input (raw: also its residual), rows of all clips
+  float* y;                // [n * t, C] x + Conv1D_b(ReLU(BN_mid(Conv1D_a(ReLU(BN_in(x)))))), y != x
+  const uint16_t* wah;     // the two Conv1D(C, 3) weights, conv_h3_split_weights layout (cin = cout = C)
+  const uint16_t* wal;
+  const uint16_t* wbh;
+  const uint16_t* wbl;
+  const float* ba;         // biases [C]
+  const float* bb;
+  const float* s_in;       // folded BatchNorms [C]: v * s + t
+  const float* t_in;
+  const float* s_mid;
+  const float* t_mid;
+  float ua, ub;            // 1 / (2^4 x the weight tensor's split scale), conv_h3's unscale
+  int n, t;                // clips, rows per clip
+  int* range_flag;         // nullable: an operand split into fp16 left the fp16 range
+};
+
+bool siu_supported(int c);
+hipError_t siu_launch(const SiuArgs& a, int c, hipStream_t stream);

@@ -1,0 +1,239 @@
+// SpeakerIdentification res_unit without pooling (speaker_identification.py:168-190; the 32- and
+// 64-channel ones, units 2-3 and 5-6 of the nine):
+//     y = x + Conv1D_b(ReLU(BN_mid(Conv1D_a(ReLU(BN_in(x))))))        Conv1D(C, 3, 'same')
+// as ONE kernel per unit.  The SI Conv1D layers run at 3-5.4 TB/s of HBM (profiles/
+// pmc_traffic_si_pipeline.json against the kernel stats): the stack is bandwidth-bound, and the
+// two-launch form moves t1 out to HBM and back (write + read) and x twice.  Here a workgroup stages
+// ROWS + 2 rows of x (BN_in + ReLU + 3xFP16 split, as conv_h3's staging), computes the ROWS rows of
+// t1 its output rows need (GEMM a), writes them back into the same LDS already BN_mid + ReLU'd and
+// split, and computes ROWS - 2 output rows (GEMM b) + bias + residual.  t1 never leaves the CU.
+//
+// Bit-identical to the conv_h3 pair it replaces: the same staged operands (values and 2^4 scale),
+// the same MFMA sequence per output element (channel chunks of 32, then taps, then k-steps, the three
+// 3xFP16 products in conv_h3's order into one accumulator), the same epilogue arithmetic, and the
+// same zero rows for taps that leave a clip (conv_h3's TW = 1 zero row) or the row sequence.
+#include "common.h"
+#include "conv.h"
+#include "siu.h"
+
+
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+
+constexpr int CK = 32;                 // channel chunk (conv_h3's k order)
+constexpr int KS = CK / 16;
+constexpr int TAPS = 3;
+constexpr float ACT_SCALE = 16.0f;
+constexpr float ACT_RANGE = 65504.0f / ACT_SCALE;
+
+MMLA_DEV float bn_relu(float v, float sc, float sh) { return fmaxf(fmaf(v, sc, sh), 0.0f); }
+
+// C channels; NW waves; ROWS = t1 rows per workgroup = a multiple of the waves' 32-row MFMA tiles;
+// output rows per workgroup R = ROWS - 2 (t1 needs one row of halo each side, x two)
+template <int C, int ROWS, int NW>
+__global__ void __launch_bounds__(64 * NW, 2) siu_kernel(SiuArgs a) {
+  constexpr int NT = 64 * NW;
+  constexpr int WN = C / 32;           // waves along N (32 columns each), as conv_h3 with BN = C
+  constexpr int WM = NW / WN;
+  constexpr int MT = ROWS / (WM * 32);
+  constexpr int NCH = C / CK;
+  constexpr int LDP = C + 8;           // fp16 per staged row (16-B pad, as conv_h3)
+  constexpr int R = ROWS - 2;
+  constexpr int XR = ROWS + 2;         // staged x rows r0 - 2 .. r0 + R + 1
+  constexpr int ZR = XR;               // the zero row (taps leaving a clip)
+  constexpr int QPP = CK / 4;          // float4 per row and chunk
+  constexpr int MAXT = (XR * QPP + NT - 1) / NT;
+  static_assert(WM * WN == NW && MT * WM * 32 == ROWS && NT % QPP == 0, "tiling");
+  __shared__ __attribute__((aligned(16))) _Float16 lhi[(XR + 1) * LDP];
+  __shared__ __attribute__((aligned(16))) _Float16 llo[(XR + 1) * LDP];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave - (wave / WN) * WN;
+  const int64_t HH = (int64_t)a.n * a.t;
+  const int64_t r0 = (int64_t)blockIdx.x * R;
+  const int koff = (lane >> 5) * 8;
+  bool rbad = false;
+
+  if (tid < LDP / 8) {   // the zero row
+    *reinterpret_cast<f16x8*>(lhi + ZR * LDP + 8 * tid) = f16x8{};
+    *reinterpret_cast<f16x8*>(llo + ZR * LDP + 8 * tid) = f16x8{};
+  }
+
+  // ---- stage x: rows r0 - 2 + j, BN_in + ReLU, x 2^4, split (all chunks, one barrier) ------------
+  {
+    const int q = tid % QPP;
+#pragma unroll 1
+    for (int ch = 0; ch < NCH; ++ch) {
+      const int ci = ch * CK + 4 * q;
+      const float4 sc = *reinterpret_cast<const float4*>(a.s_in + ci);
+      const float4 sh = *reinterpret_cast<const float4*>(a.t_in + ci);
+      float4 pre[MAXT];
+      uint32_t valid = 0;
+#pragma unroll
+      for (int j = 0; j < MAXT; ++j) {
+        const int task = tid + j * NT;
+        pre[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+        const int64_t g = r0 - 2 + task / QPP;
+        if (task < XR * QPP && g >= 0 && g < HH) {
+          pre[j] = *reinterpret_cast<const float4*>(a.x + g * C + ci);
+          valid |= 1u << j;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < MAXT; ++j) {
+        const int task = tid + j * NT;
+        if (task >= XR * QPP) continue;
+        float4 v = pre[j];
+        if (valid & (1u << j)) {
+          v.x = bn_relu(v.x, sc.x, sh.x);
+          v.y = bn_relu(v.y, sc.y, sh.y);
+          v.z = bn_relu(v.z, sc.z, sh.z);
+          v.w = bn_relu(v.w, sc.w, sh.w);
+        }
+        rbad |= !(fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))) < ACT_RANGE);
+        v.x *= ACT_SCALE;
+        v.y *= ACT_SCALE;
+        v.z *= ACT_SCALE;
+        v.w *= ACT_SCALE;
+        f16x4 hv, lv;
+        hv[0] = (_Float16)v.x;
+        hv[1] = (_Float16)v.y;
+        hv[2] = (_Float16)v.z;
+        hv[3] = (_Float16)v.w;
+        lv[0] = (_Float16)(v.x - (float)hv[0]);
+        lv[1] = (_Float16)(v.y - (float)hv[1]);
+        lv[2] = (_Float16)(v.z - (float)hv[2]);
+        lv[3] = (_Float16)(v.w - (float)hv[3]);
+        const int row = task / QPP;
+        *reinterpret_cast<f16x4*>(lhi + row * LDP + ci) = hv;
+        *reinterpret_cast<f16x4*>(llo + row * LDP + ci) = lv;
+      }
+    }
+  }
+  __syncthreads();
+
+  // B fragments (conv_h3_split_weights order): per tap, 16-channel k-step and 32-column tile
+  constexpr size_t tap_stride = (size_t)C * C;
+  constexpr size_t kstride = (size_t)(C / 32) * 512;
+  const int lofs = wn * 512 + lane * 8;
+  // this lane's A rows and, per tap, the LDS row it reads (the zero row where the tap leaves the clip)
+  auto gemm = [&](const uint16_t* __restrict__ wh, const uint16_t* __restrict__ wl, int64_t g_row0,
+                  f32x16 (&acc)[MT]) {
+    int mrow[MT], trow[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      mrow[mt] = (wm * MT + mt) * 32 + (lane & 31);
+      const int64_t g = g_row0 + mrow[mt];                 // the global row of this A row
+      trow[mt] = (int)(((g % a.t) + a.t) % a.t);           // its position in its clip
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[mt][i] = 0.0f;
+    }
+#pragma unroll 1
+    for (int ch = 0; ch < NCH; ++ch) {
+#pragma unroll 1
+      for (int tap = 0; tap < TAPS; ++tap) {   // (unrolled, every tap's A reads were hoisted: spills)
+        f16x8 bh[KS], bl[KS];
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+          const size_t u = tap * tap_stride + (size_t)(ch * KS + s) * kstride + lofs;
+          bh[s] = *reinterpret_cast<const f16x8*>(wh + u);
+          bl[s] = *reinterpret_cast<const f16x8*>(wl + u);
+        }
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt) {
+            const int src = trow[mt] + tap - 1;
+            const int off = (src < 0 || src >= a.t ? ZR : mrow[mt] + tap) * LDP + ch * CK + 16 * s + koff;
+            const f16x8 ah = *reinterpret_cast<const f16x8*>(lhi + off);
+            const f16x8 al = *reinterpret_cast<const f16x8*>(llo + off);
+            acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl[s], acc[mt], 0, 0, 0);
+            acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[s], acc[mt], 0, 0, 0);
+            acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[s], acc[mt], 0, 0, 0);
+          }
+      }
+    }
+  };
+
+  const int co = wn * 32 + (lane & 31);
+  const int hsel = 4 * (lane >> 5);
+  f32x16 acc[MT];
+  // ---- GEMM a: t1 rows r0 - 1 + m, m < ROWS (x LDS row of t1 row m at tap dy: m + dy) -------------
+  gemm(a.wah, a.wal, r0 - 1, acc);
+  __syncthreads();   // every wave has read x
+  {
+    const float b = a.ba[co], s2 = a.s_mid[co], t2 = a.t_mid[co];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = (wm * MT + mt) * 32 + (r & 3) + 8 * (r >> 2) + hsel;
+        const int64_t g = r0 - 1 + m;
+        float v = 0.0f;
+        if (g >= 0 && g < HH) {   // rows outside the sequence stage as zeros (conv_h3's valid mask)
+          v = bn_relu(fmaf(acc[mt][r], a.ua, b), s2, t2);
+          rbad |= !(fabsf(v) < ACT_RANGE);
+        }
+        v *= ACT_SCALE;
+        const _Float16 hv = (_Float16)v;
+        lhi[m * LDP + co] = hv;
+        llo[m * LDP + co] = (_Float16)(v - (float)hv);
+      }
+  }
+  __syncthreads();
+  // ---- GEMM b: output rows r0 + m, m < R (t1 LDS row of output row m at tap dy: m + dy) -----------
+  gemm(a.wbh, a.wbl, r0, acc);
+  {
+    const float b = a.bb[co];
+    float rsd[MT][16];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = (wm * MT + mt) * 32 + (r & 3) + 8 * (r >> 2) + hsel;
+        const int64_t g = r0 + m;
+        rsd[mt][r] = m < R && g < HH ? a.x[g * C + co] : 0.0f;
+      }
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = (wm * MT + mt) * 32 + (r & 3) + 8 * (r >> 2) + hsel;
+        const int64_t g = r0 + m;
+        if (m < R && g < HH) {
+          float val = fmaf(acc[mt][r], a.ub, b);
+          val += rsd[mt][r];
+          a.y[g * C + co] = val;
+        }
+      }
+  }
+  if (rbad && a.range_flag) *a.range_flag = 1;
+}
+
+template <int C, int ROWS, int NW>
+hipError_t launch(const SiuArgs& a, hipStream_t s) {
+  const int64_t rows = (int64_t)a.n * a.t;
+  const int64_t blocks = (rows + (ROWS - 2) - 1) / (ROWS - 2);
+  hipLaunchKernelGGL((siu_kernel<C, ROWS, NW>), dim3((unsigned)blocks), dim3(64 * NW), 0, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+bool siu_supported(int c) { return c == 32 || c == 64; }
+
+hipError_t siu_launch(const SiuArgs& a, int c, hipStream_t s) {
+  if ((int64_t)a.n * a.t == 0) return hipSuccess;
+  if (!a.x || !a.y || a.x == a.y || a.t < 1) return hipErrorInvalidValue;
+  // two 32-row MFMA tiles per wave (no spills), 3 workgroups per CU.  Measured per unit and SI step
+  // (rocprof, 65 536 clips) against the conv_h3 pair it replaces: C = 32 1.004 vs 1.033 ms, C = 64
+  // 1.061 vs 1.203 ms; C = 128 (64-row tiles: the B fragments streamed per 62 output rows) 1.672 vs
+  // 1.625 ms -- the 128-channel units keep the pair.  Tried: 8-wave workgroups with 256 / 128 t1 rows
+  // for C = 64 / 128 (one workgroup per CU) and 512-row tiles for C = 32 (occupancy 1): slower
+  if (c == 32) return launch<32, 256, 4>(a, s);
+  if (c == 64) return launch<64, 128, 4>(a, s);
+  return hipErrorInvalidValue;
+}
