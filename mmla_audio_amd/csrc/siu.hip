@@ -1,5 +1,5 @@
-// SpeakerIdentification res_unit without pooling (speaker_identification.py:168-190; the 32- and
-// 64-channel ones, units 2-3 and 5-6 of the nine):
+// SpeakerIdentification res_unit without pooling (speaker_identification.py:168-190; units 2-3, 5-6,
+// 8-9 of the nine):
 //     y = x + Conv1D_b(ReLU(BN_mid(Conv1D_a(ReLU(BN_in(x))))))        Conv1D(C, 3, 'same')
 // as ONE kernel per unit.  The SI Conv1D layers run at 3-5.4 TB/s of HBM (profiles/
 // pmc_traffic_si_pipeline.json against the kernel stats): the stack is bandwidth-bound, and the
@@ -16,6 +16,10 @@
 #include "conv.h"
 #include "siu.h"
 
+
+#ifndef SIU_MT4
+#define SIU_MT4 1
+#endif
 
 namespace {
 
@@ -188,27 +192,26 @@ __global__ void __launch_bounds__(64 * NW, 2) siu_kernel(SiuArgs a) {
   gemm(a.wbh, a.wbl, r0, acc);
   {
     const float b = a.bb[co];
-    float rsd[MT][16];
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
+    for (int mt = 0; mt < MT; ++mt) {   // one 32-row tile at a time: 16 residuals live, not 16 MT
+      float rsd[16];
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int m = (wm * MT + mt) * 32 + (r & 3) + 8 * (r >> 2) + hsel;
         const int64_t g = r0 + m;
-        rsd[mt][r] = m < R && g < HH ? a.x[g * C + co] : 0.0f;
+        rsd[r] = m < R && g < HH ? a.x[g * C + co] : 0.0f;
       }
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int m = (wm * MT + mt) * 32 + (r & 3) + 8 * (r >> 2) + hsel;
         const int64_t g = r0 + m;
         if (m < R && g < HH) {
           float val = fmaf(acc[mt][r], a.ub, b);
-          val += rsd[mt][r];
+          val += rsd[r];
           a.y[g * C + co] = val;
         }
       }
+    }
   }
   if (rbad && a.range_flag) *a.range_flag = 1;
 }
@@ -223,17 +226,24 @@ hipError_t launch(const SiuArgs& a, hipStream_t s) {
 
 }  // namespace
 
-bool siu_supported(int c) { return c == 32 || c == 64; }
+bool siu_supported(int c) { return c == 32 || c == 64 || (SIU_MT4 && c == 128); }
 
 hipError_t siu_launch(const SiuArgs& a, int c, hipStream_t s) {
   if ((int64_t)a.n * a.t == 0) return hipSuccess;
   if (!a.x || !a.y || a.x == a.y || a.t < 1) return hipErrorInvalidValue;
-  // two 32-row MFMA tiles per wave (no spills), 3 workgroups per CU.  Measured per unit and SI step
-  // (rocprof, 65 536 clips) against the conv_h3 pair it replaces: C = 32 1.004 vs 1.033 ms, C = 64
-  // 1.061 vs 1.203 ms; C = 128 (64-row tiles: the B fragments streamed per 62 output rows) 1.672 vs
-  // 1.625 ms -- the 128-channel units keep the pair.  Tried: 8-wave workgroups with 256 / 128 t1 rows
-  // for C = 64 / 128 (one workgroup per CU) and 512-row tiles for C = 32 (occupancy 1): slower
+  // Tiles (4 waves): C = 32 256 t1 rows (MT 2, 134 VGPRs, 3 workgroups per CU); C = 64 256 rows and
+  // C = 128 128 rows (MT 4, 242 VGPRs once the residual epilogue went tile by tile, 2 per CU).
+  // Measured per unit and SI step against the conv_h3 pair: C = 32 1.004 vs 1.033 ms, C = 64 (128-row
+  // tiles) 1.061 vs 1.203 ms, C = 128 with 64-row tiles 1.672 vs 1.625 ms (B streamed per 62 output
+  // rows); with the MT 4 tiles SI 2.45 -> 2.51 M clips/s (A/B, 2 rounds; the conv stage itself
+  // +0.8 %).  SIU_MT4=0: the 128-row C = 64 tiles, C = 128 on the pair.  Tried: 8-wave workgroups
+  // (one per CU) and 512-row C = 32 tiles (occupancy 1): slower
   if (c == 32) return launch<32, 256, 4>(a, s);
+#if SIU_MT4
+  if (c == 64) return launch<64, 256, 4>(a, s);
+  if (c == 128) return launch<128, 128, 4>(a, s);
+#else
   if (c == 64) return launch<64, 128, 4>(a, s);
+#endif
   return hipErrorInvalidValue;
 }
