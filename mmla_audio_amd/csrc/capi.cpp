@@ -129,6 +129,10 @@ struct mmla_ctx {
   // SI res units without pooling as one fused kernel each (siu.hip); env MMLA_NO_SIU=1 at create:
   // the two conv_h3 launches (A/B)
   bool siu = true;
+  // ... and the pool units too (siu.hip POOL); env MMLA_NO_SIPU=0 / 1 at create
+  bool sipu = false;
+  // ... and the last one with the final BN + ReLU + AvgPool4 (siu.hip FIN); env MMLA_NO_SIFIN=0 / 1
+  bool sifin = false;
   // 3xFP16 range guard: kernels set range_dev[0] (device-pointer calls; sticky until
   // mmla_range_check) or range_dev[1] (host-pointer micro-batches: re-run in exact f32) when an
   // operand they split into fp16 is >= 65504 in magnitude or not finite
@@ -894,12 +898,48 @@ int run_si_net(mmla_ctx* c, const float* x, int64_t n, float* probs, int32_t* ar
   float* XP = static_cast<float*>(pt2);
   float* R = static_cast<float*>(pt3);
   int t = SI_T;
+  bool fused_final = false;   // the last unit wrote BN + ReLU + AvgPool4 itself (siu FIN)
   // Conv1D(32, 4, same): [n, 256, 1, 39] -> [n, 256, 1, 32] (speaker_identification.py:195)
   CHK(conv_spatial(c, W.stem, x, X, (int)n, t, 1, nullptr, PRO_NONE, EPI_BIAS, nullptr));
   for (int u = 0; u < 9; ++u) {   // res_unit, speaker_identification.py:168-190
     const SiUnit& U = W.unit[u];
     const int cin = U.ca.cin;
-    if (POOL[u]) {
+    if (POOL[u] && c->siu && c->sipu && c->precision == MMLA_PREC_F16X3 && U.ca.wh && U.cb.wh && U.sc.wh &&
+        sipu_supported(cin, U.ca.cout) && U.ca.cin_pad == cin && U.ca.cout_pad == U.ca.cout &&
+        U.cb.cin == U.ca.cout && U.cb.cout == U.ca.cout && U.cb.cout_pad == U.ca.cout &&
+        U.sc.cin == cin && U.sc.cout == U.ca.cout && U.sc.cout_pad == U.ca.cout) {
+      // the whole pool unit in one launch: MaxPool1D in the staging, t1 on chip, the shortcut in the
+      // epilogue (siu.hip POOL), bit-identical to the two conv_h3 launches below
+      const int tp = (t + 1) / 2;
+      SiuArgs s{};
+      s.x = X;
+      s.y = R;
+      s.wah = U.ca.wh;
+      s.wal = U.ca.wl;
+      s.wbh = U.cb.wh;
+      s.wbl = U.cb.wl;
+      s.ba = U.ca.bias;
+      s.bb = U.cb.bias;
+      s.s_in = U.bn_in.scale;
+      s.t_in = U.bn_in.shift;
+      s.s_mid = U.bn_mid.scale;
+      s.t_mid = U.bn_mid.shift;
+      s.ua = U.ca.unscale();
+      s.ub = U.cb.unscale();
+      s.n = (int)n;
+      s.t = tp;
+      s.t_src = t;
+      s.wsh = U.sc.wh;
+      s.wsl = U.sc.wl;
+      s.bs = U.sc.bias;
+      s.us = U.sc.unscale();
+      s.range_flag = c->range_ptr;
+      const double C = U.ca.cout;
+      LAUNCH(c, MMLA_STAGE_CONV, 2.0 * n * tp * (3.0 * cin * C + 3.0 * C * C + cin * C),
+             sipu_launch(s, cin, U.ca.cout, c->stream));
+      std::swap(X, R);
+      t = tp;
+    } else if (POOL[u]) {
       const int tp = (t + 1) / 2;
       if (c->precision == MMLA_PREC_F16X3 && U.ca.wh) {
         // MaxPool1D(2, same) taken inside the conv's staging (conv_h3.hip PIN)
@@ -943,6 +983,15 @@ int run_si_net(mmla_ctx* c, const float* x, int64_t n, float* probs, int32_t* ar
       s.n = (int)n;
       s.t = t;
       s.range_flag = c->range_ptr;
+      if (u == 8 && c->sifin && siu_final_supported(cin) && cin == 128 && t % 4 == 0) {
+        // + the final BN + ReLU + AveragePooling1D(4) in the epilogue: the unit's output never
+        // reaches HBM (bit-identical to bn_relu_avgpool4_launch below)
+        s.y = nullptr;
+        s.seq = static_cast<float*>(pseq);
+        s.fs = W.final_bn.scale;
+        s.ft = W.final_bn.shift;
+        fused_final = true;
+      }
       LAUNCH(c, MMLA_STAGE_CONV, 2.0 * 2.0 * n * t * 3 * cin * cin, siu_launch(s, cin, c->stream));
       std::swap(X, R);
     } else {
@@ -951,9 +1000,10 @@ int run_si_net(mmla_ctx* c, const float* x, int64_t n, float* probs, int32_t* ar
     }
   }
   // t = 32, c = 128 -> BN -> ReLU -> AvgPool1D(4) -> [n, 8, 128] (speaker_identification.py:208-212)
-  LAUNCH(c, MMLA_STAGE_GLUE, 3.0 * n * t * 128,
-         bn_relu_avgpool4_launch(X, (int)n, t, 128, W.final_bn.scale, W.final_bn.shift,
-                                 static_cast<float*>(pseq), c->stream));
+  if (!fused_final)
+    LAUNCH(c, MMLA_STAGE_GLUE, 3.0 * n * t * 128,
+           bn_relu_avgpool4_launch(X, (int)n, t, 128, W.final_bn.scale, W.final_bn.shift,
+                                   static_cast<float*>(pseq), c->stream));
   LAUNCH(c, MMLA_STAGE_LSTM, lstm_flops(n, t / 4, 128),
          lstm_run(c, W.lstm, static_cast<float*>(pseq), n, t / 4, static_cast<float*>(ph)));
   if (c->precision == MMLA_PREC_F16X3 && W.dense.wh && W.dense.cin % 32 == 0) {
@@ -1029,6 +1079,8 @@ int mmla_create(int device, mmla_ctx** out) {
   c->device = device;
   if (const char* fa = std::getenv("MMLA_DEBUG_FAIL_ALLOC")) c->debug_fail_allocs = std::atoi(fa);
   if (const char* su = std::getenv("MMLA_NO_SIU")) c->siu = std::atoi(su) == 0;
+  if (const char* sp = std::getenv("MMLA_NO_SIPU")) c->sipu = std::atoi(sp) == 0;
+  if (const char* sf = std::getenv("MMLA_NO_SIFIN")) c->sifin = std::atoi(sf) == 0;
   // a BLOCKING stream: it orders with the legacy default (NULL) stream, on which PyTorch's default
   // stream enqueues -- so a device-pointer call sees tensors a torch kernel or copy just produced
   // without an explicit synchronisation (a non-blocking stream raced them: a 65 536-clip call read

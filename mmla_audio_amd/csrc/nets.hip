@@ -201,8 +201,14 @@ MMLA_DEV void split1(float v, _Float16& h, _Float16& l) {   // v * 2^6 = hi + lo
 
 // MT 32-clip row tiles per workgroup (1, or 2 where the batch still fills the chip: half the weight
 // stream per clip); PF: prefetch the next k-step's B fragments (MT 1 only: registers)
+// LSTM_W4: two workgroups per CU (4 waves per SIMD, <= 128 VGPRs): each k-step's B fragments loaded
+// gate by gate right before their MFMAs (no prefetch ring), the other workgroup's waves hiding the
+// L2 latency instead
+#ifndef LSTM_W4
+#define LSTM_W4 0
+#endif
 template <int D, int MT>
-__global__ void __launch_bounds__(512) bilstm_h3_kernel(const float* __restrict__ seq, int n, int T,
+__global__ void __launch_bounds__(512, (LSTM_W4 && MT == 1) ? 4 : 2) bilstm_h3_kernel(const float* __restrict__ seq, int n, int T,
                                                         const uint16_t* __restrict__ wfh,
                                                         const uint16_t* __restrict__ wfl,
                                                         const uint16_t* __restrict__ wbh,
@@ -217,7 +223,8 @@ __global__ void __launch_bounds__(512) bilstm_h3_kernel(const float* __restrict_
   constexpr int LDA = K + 8;             // fp16 per A row (16-B pad)
   constexpr int NTH = 512;
   constexpr int ROWS = 32 * MT;
-  constexpr bool PF = MT == 1;
+  constexpr bool W4 = LSTM_W4 && MT == 1;
+  constexpr bool PF = MT == 1 && !W4;
   __shared__ __attribute__((aligned(16))) _Float16 Ahi[ROWS * LDA];
   __shared__ __attribute__((aligned(16))) _Float16 Alo[ROWS * LDA];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -290,6 +297,41 @@ __global__ void __launch_bounds__(512) bilstm_h3_kernel(const float* __restrict_
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[mt][g][r] = bv;
     }
+    if constexpr (W4 && LSTM_W4 == 2) {
+      // one gate ahead: the next (k-step, gate)'s B fragments in flight under this gate's MFMAs
+      f16x8 gh = *reinterpret_cast<const f16x8*>(wh0);
+      f16x8 gl = *reinterpret_cast<const f16x8*>(wl0);
+#pragma unroll 1
+      for (int ks = 0; ks < KST; ++ks) {
+        const f16x8 ah = *reinterpret_cast<const f16x8*>(arow_h + 16 * ks);
+        const f16x8 al = *reinterpret_cast<const f16x8*>(arow_l + 16 * ks);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int gn = g < 3 ? g + 1 : 0, kn = g < 3 ? ks : (ks + 1 < KST ? ks + 1 : ks);
+          const f16x8 nh = *reinterpret_cast<const f16x8*>(wh0 + gn * GS + 512 * kn);
+          const f16x8 nl = *reinterpret_cast<const f16x8*>(wl0 + gn * GS + 512 * kn);
+          acc[0][g] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, gh, acc[0][g], 0, 0, 0);
+          acc[0][g] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, gl, acc[0][g], 0, 0, 0);
+          acc[0][g] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, gh, acc[0][g], 0, 0, 0);
+          gh = nh;
+          gl = nl;
+        }
+      }
+    } else if constexpr (W4) {
+#pragma unroll 1
+      for (int ks = 0; ks < KST; ++ks) {
+        const f16x8 ah = *reinterpret_cast<const f16x8*>(arow_h + 16 * ks);
+        const f16x8 al = *reinterpret_cast<const f16x8*>(arow_l + 16 * ks);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const f16x8 gh = *reinterpret_cast<const f16x8*>(wh0 + g * GS + 512 * ks);
+          const f16x8 gl = *reinterpret_cast<const f16x8*>(wl0 + g * GS + 512 * ks);
+          acc[0][g] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, gh, acc[0][g], 0, 0, 0);
+          acc[0][g] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, gl, acc[0][g], 0, 0, 0);
+          acc[0][g] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, gh, acc[0][g], 0, 0, 0);
+        }
+      }
+    } else
 #pragma unroll 2
     for (int ks = 0; ks < KST; ++ks) {
       f16x8 nh[4], nl[4];
@@ -340,7 +382,9 @@ __global__ void __launch_bounds__(512) bilstm_h3_kernel(const float* __restrict_
         cst[mt][r] = c;
         const float h = og * tanh_f(c);
         if (s == T - 1) {   // the last state (Keras return_sequences=False), float32
-          const int64_t clip = c0 + row;
+          int rr = row;
+          asm volatile("" : "+v"(rr));   // the address formed here: hoisted, 16 of them were spilled
+          const int64_t clip = c0 + rr;
           if (clip < n) out[clip * 512 + dir * LSTM_U + col] = h;
         }
         _Float16 hh, hl;

@@ -17,9 +17,24 @@ struct SiuArgs {
   const float* s_mid;
   const float* t_mid;
   float ua, ub;            // 1 / (2^4 x the weight tensor's split scale), conv_h3's unscale
-  int n, t;                // clips, rows per clip
+  int n, t;                // clips, rows per clip (pool units: pooled rows, (t_src + 1) / 2)
   int* range_flag;         // nullable: an operand split into fp16 left the fp16 range
+  // pool units only (sipu_launch): x is [n * t_src, CIN]; the shortcut Conv1D(C, 1, strides=2)
+  int t_src;
+  const uint16_t* wsh;     // its weight, conv_h3_split_weights layout (cin = CIN, cout = C)
+  const uint16_t* wsl;
+  const float* bs;         // its bias [C]
+  float us;                // its unscale
+  // siu_launch with seq set (the last unit, siu_final_supported): instead of y, seq [n * t / 4, C] =
+  // AveragePooling1D(4)(ReLU(x_out * fs + ft)) (the final BatchNormalization, folded)
+  float* seq;
+  const float* fs;
+  const float* ft;
 };
 
 bool siu_supported(int c);
+bool siu_final_supported(int c);
 hipError_t siu_launch(const SiuArgs& a, int c, hipStream_t stream);
+// the pool unit (speaker_identification.py:170-172 + 173-188) with t1 kept on chip
+bool sipu_supported(int cin, int c);
+hipError_t sipu_launch(const SiuArgs& a, int cin, int c, hipStream_t stream);

@@ -1,6 +1,10 @@
-"""The fused SI res unit (siu.hip: Conv1D -> BN -> ReLU -> Conv1D + residual in one launch, t1 kept in
-LDS) against the two conv_h3 launches it replaces: bit-identical SI probabilities over a batch with
-ragged and 'silent' clips, across several tiles and clip boundaries (MMLA_NO_SIU=1 selects the pair)."""
+"""The fused SI res units (siu.hip) against the conv_h3 launches they replace: bit-identical SI
+probabilities over a batch with ragged and 'silent' clips, across several tiles and clip boundaries.
+
+* MMLA_NO_SIU: units without pooling (Conv1D -> BN -> ReLU -> Conv1D + residual, t1 kept in LDS);
+* MMLA_NO_SIPU: the pool units (MaxPool1D in the staging, the stride-2 shortcut in the epilogue);
+* MMLA_NO_SIFIN: the last unit writing the final BN + ReLU + AveragePooling1D(4) itself.
+Each switch is set explicitly, so the tests hold whatever the library's defaults are."""
 import numpy as np
 import pytest
 
@@ -8,21 +12,42 @@ from oracle import synth
 
 pytestmark = pytest.mark.gpu
 
+ALL_ON = {'MMLA_NO_SIU': '0', 'MMLA_NO_SIPU': '0', 'MMLA_NO_SIFIN': '0'}
+ALL_OFF = {'MMLA_NO_SIU': '1', 'MMLA_NO_SIPU': '1', 'MMLA_NO_SIFIN': '1'}
 
-def _ctx(monkeypatch, fused):
+
+def _ctx(monkeypatch, env):
     from mmla_audio_amd import _lib, weights
-    monkeypatch.setenv('MMLA_NO_SIU', '0' if fused else '1')
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
     c = _lib.Context(0)
-    monkeypatch.delenv('MMLA_NO_SIU')
+    for k in env:
+        monkeypatch.delenv(k)
     W = weights.synthetic(weights.SI, seed=31, n_classes=630)
     c.load_weights(weights.SI, weights.pack(weights.SI, W, 630), 630, _lib.HEAD_SOFTMAX)
     return c
 
 
-def test_fused_units_bit_identical(monkeypatch):
+@pytest.fixture(scope='module')
+def pcm():
     lens = [24000 if i % 9 else (3000 if i % 2 else 17000) for i in range(300)]
-    pcm = [synth.clip(4000 + i, n) for i, n in enumerate(lens)]
-    p_pair, a_pair, s_pair = _ctx(monkeypatch, False).si_pipeline(pcm)
-    p_fused, a_fused, s_fused = _ctx(monkeypatch, True).si_pipeline(pcm)
-    assert np.array_equal(p_fused, p_pair) and np.array_equal(a_fused, a_pair)
-    assert np.array_equal(s_fused, s_pair)
+    return [synth.clip(4000 + i, n) for i, n in enumerate(lens)]
+
+
+def _same(monkeypatch, pcm, env_a, env_b):
+    p_a, a_a, s_a = _ctx(monkeypatch, env_a).si_pipeline(pcm)
+    p_b, a_b, s_b = _ctx(monkeypatch, env_b).si_pipeline(pcm)
+    assert np.array_equal(p_a, p_b) and np.array_equal(a_a, a_b)
+    assert np.array_equal(s_a, s_b)
+
+
+def test_fused_units_bit_identical(monkeypatch, pcm):
+    _same(monkeypatch, pcm, ALL_ON, ALL_OFF)
+
+
+def test_fused_pool_units_bit_identical(monkeypatch, pcm):
+    _same(monkeypatch, pcm, ALL_ON, dict(ALL_ON, MMLA_NO_SIPU='1'))
+
+
+def test_fused_final_pool_bit_identical(monkeypatch, pcm):
+    _same(monkeypatch, pcm, ALL_ON, dict(ALL_ON, MMLA_NO_SIFIN='1'))
