@@ -129,10 +129,11 @@ struct mmla_ctx {
   // SI res units without pooling as one fused kernel each (siu.hip); env MMLA_NO_SIU=1 at create:
   // the two conv_h3 launches (A/B)
   bool siu = true;
-  // ... and the pool units too (siu.hip POOL); env MMLA_NO_SIPU=0 / 1 at create
-  bool sipu = false;
-  // ... and the last one with the final BN + ReLU + AvgPool4 (siu.hip FIN); env MMLA_NO_SIFIN=0 / 1
-  bool sifin = false;
+  // ... and the pool units too (siu.hip POOL); env MMLA_NO_SIPU=1 at create: the conv_h3 pair
+  bool sipu = true;
+  // ... and the last one with the final BN + ReLU + AvgPool4 (siu.hip FIN); env MMLA_NO_SIFIN=1: the
+  // unit writes its output and bn_relu_avgpool4 runs as its own launch
+  bool sifin = true;
   // 3xFP16 range guard: kernels set range_dev[0] (device-pointer calls; sticky until
   // mmla_range_check) or range_dev[1] (host-pointer micro-batches: re-run in exact f32) when an
   // operand they split into fp16 is >= 65504 in magnitude or not finite

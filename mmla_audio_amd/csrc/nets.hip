@@ -201,11 +201,14 @@ MMLA_DEV void split1(float v, _Float16& h, _Float16& l) {   // v * 2^6 = hi + lo
 
 // MT 32-clip row tiles per workgroup (1, or 2 where the batch still fills the chip: half the weight
 // stream per clip); PF: prefetch the next k-step's B fragments (MT 1 only: registers)
-// LSTM_W4: two workgroups per CU (4 waves per SIMD, <= 128 VGPRs): each k-step's B fragments loaded
-// gate by gate right before their MFMAs (no prefetch ring), the other workgroup's waves hiding the
-// L2 latency instead
+// LSTM_W4 (round 4): two workgroups per CU (4 waves per SIMD, <= 128 VGPRs) instead of one with a
+// k-step-ahead B ring at 242 VGPRs.  2 (the product): B fragments one GATE ahead (the next
+// (k-step, gate)'s 2 x 16 B in flight under this gate's 3 MFMAs); 1: loaded right before their MFMAs,
+// the other workgroup's waves hiding the L2 latency.  Bit-identical to 0 (same MFMA order per
+// accumulator).  Measured (A/B, one box): SI LSTM stage 9.36 -> 8.71 ms per 3 steps (2) / 9.31 (1);
+// OD LSTM 23.8 -> 21.7 ms per 3 steps (2); SI 2.63 -> 2.65 M clips/s
 #ifndef LSTM_W4
-#define LSTM_W4 0
+#define LSTM_W4 2
 #endif
 template <int D, int MT>
 __global__ void __launch_bounds__(512, (LSTM_W4 && MT == 1) ? 4 : 2) bilstm_h3_kernel(const float* __restrict__ seq, int n, int T,
