@@ -5,6 +5,7 @@
 //   hipcc --offload-arch=gfx950 -O3 -o valu_rates valu_rates.hip && ./valu_rates 2100
 #include <hip/hip_runtime.h>
 #include <cstdio>
+#include <cstdint>
 #include <cstdlib>
 
 constexpr int ITERS = 4096;
@@ -42,7 +43,10 @@ __global__ void __launch_bounds__(256) rate_kernel(float* out, double* outd, flo
     const float m = 0.999999f + s * 1e-12f, k = 1e-7f;
     for (int i = 0; i < ITERS; ++i)
 #pragma unroll
-      for (int c = 0; c < CH; ++c) a[c] = __builtin_fmaf(a[c], m, k);
+      for (int c = 0; c < CH; ++c) {
+        a[c] = __builtin_fmaf(a[c], m, k);
+        asm volatile("" : "+v"(a[c]));   // one chain per register: no v_pk_fma_f32 pairing
+      }
     float r = 0;
     for (int c = 0; c < CH; ++c) r += a[c];
     out[t] = r;
@@ -70,12 +74,62 @@ __global__ void __launch_bounds__(256) rate_kernel(float* out, double* outd, flo
     double r = 0;
     for (int c = 0; c < CH; ++c) r += a[c];
     outd[t] = r;
-  } else {   // v_exp_f32
+  } else if constexpr (KIND == 6) {   // v_add_u32 (+ v_xor via the chain mix)
+    uint32_t a[CH];
+    for (int c = 0; c < CH; ++c) a[c] = t * 7 + c;
+    const uint32_t k = 0x9e3779b9u + (uint32_t)s;
+    for (int i = 0; i < ITERS; ++i)
+#pragma unroll
+      for (int c = 0; c < CH; ++c) {
+        a[c] = a[c] + k;
+        asm volatile("" : "+v"(a[c]));
+      }
+    uint32_t r = 0;
+    for (int c = 0; c < CH; ++c) r ^= a[c];
+    out[t] = (float)r;
+  } else if constexpr (KIND == 7) {   // v_perm_b32
+    uint32_t a[CH];
+    for (int c = 0; c < CH; ++c) a[c] = t * 7 + c;
+    const uint32_t k = 0x01234567u + (uint32_t)s;
+    for (int i = 0; i < ITERS; ++i)
+#pragma unroll
+      for (int c = 0; c < CH; ++c) a[c] = __builtin_amdgcn_perm(a[c], k, 0x05010400u);
+    uint32_t r = 0;
+    for (int c = 0; c < CH; ++c) r ^= a[c];
+    out[t] = (float)r;
+  } else if constexpr (KIND == 8) {   // v_cvt_pk_f16_f32 (f32 pair -> packed f16), chained through a bitcast
+    float a[CH];
+    for (int c = 0; c < CH; ++c) a[c] = t * 1e-3f + c;
+    for (int i = 0; i < ITERS; ++i)
+#pragma unroll
+      for (int c = 0; c < CH; ++c) {
+        typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+        typedef float fl2 __attribute__((ext_vector_type(2)));
+        const h2 h = __builtin_convertvector((fl2{a[c], a[c]}), h2);
+        a[c] = __builtin_bit_cast(float, h);
+      }
+    float r = 0;
+    for (int c = 0; c < CH; ++c) r += a[c];
+    out[t] = r;
+  } else if constexpr (KIND == 9) {   // v_dot4_i32_i8
+    int a[CH];
+    for (int c = 0; c < CH; ++c) a[c] = t * 7 + c;
+    const int k = 0x01020304 + (int)s;
+    for (int i = 0; i < ITERS; ++i)
+#pragma unroll
+      for (int c = 0; c < CH; ++c) a[c] = __builtin_amdgcn_sdot4(a[c], k, a[c], false);
+    int r = 0;
+    for (int c = 0; c < CH; ++c) r ^= a[c];
+    out[t] = (float)r;
+  } else {   // v_exp_f32 + v_sub_f32
     float a[CH];
     for (int c = 0; c < CH; ++c) a[c] = -(t & 7) * 0.1f - c * 0.01f;
     for (int i = 0; i < ITERS; ++i)
 #pragma unroll
-      for (int c = 0; c < CH; ++c) a[c] = __builtin_amdgcn_exp2f(a[c]) - 1.0f;
+      for (int c = 0; c < CH; ++c) {
+        a[c] = __builtin_amdgcn_exp2f(a[c]) - 1.0f;
+        asm volatile("" : "+v"(a[c]));
+      }
     float r = 0;
     for (int c = 0; c < CH; ++c) r += a[c];
     out[t] = r;
@@ -123,6 +177,10 @@ int main(int argc, char** argv) {
   run<1>("v_add_f64", cus, o, od, mhz, 1);
   run<4>("v_mul_f64", cus, o, od, mhz, 1);
   run<5>("v_exp_f32+sub", cus, o, od, mhz, 1);
+  run<6>("v_add_u32", cus, o, od, mhz, 1);
+  run<7>("v_perm_b32", cus, o, od, mhz, 1);
+  run<8>("v_cvt_pk_f16_f32", cus, o, od, mhz, 1);
+  run<9>("v_dot4_i32_i8", cus, o, od, mhz, 1);
   hipFree(o);
   hipFree(od);
   return 0;
