@@ -187,8 +187,30 @@ typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 
 // gate nonlinearities on the hardware exp / rcp (a few ulp from expf / tanhf; far inside the 1e-4
 // probability tolerance)
-MMLA_DEV float sigm_f(float z) { return __frcp_rn(1.0f + __expf(-z)); }
-MMLA_DEV float tanh_f(float x) { return 1.0f - 2.0f * __frcp_rn(1.0f + __expf(2.0f * x)); }
+// LSTM_RCP 1: v_rcp_f32 (1 ulp) for the reciprocal; 0: __frcp_rn, correctly rounded, which compiles to
+// the ~10-instruction IEEE division sequence -- 80 of them per lane and step sit between a step's
+// last MFMA and its barrier
+#ifndef LSTM_RCP
+#define LSTM_RCP 1
+#endif
+MMLA_DEV float lstm_rcp(float x) {
+#if LSTM_RCP
+  return __builtin_amdgcn_rcpf(x);
+#else
+  return __frcp_rn(x);
+#endif
+}
+MMLA_DEV float sigm_f(float z) { return lstm_rcp(1.0f + __expf(-z)); }
+MMLA_DEV float tanh_f(float x) { return 1.0f - 2.0f * lstm_rcp(1.0f + __expf(2.0f * x)); }
+
+// raw buffer descriptor over [p, p + bytes) for a wave-uniform p (SGPRs), as od_fe.hip wave_rsrc
+MMLA_DEV __amdgpu_buffer_rsrc_t lstm_rsrc(const void* p, uint32_t bytes) {
+  const uint64_t u = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)u);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(u >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), (short)0,
+                                           (int)bytes, 0x00020000);
+}
 
 // weights: a per-direction power-of-two scale ws (bilstm_h3_split_weights; capi.cpp pick_wscale)
 constexpr float LSTM_AS = 64.0f;    // [h | x] scale
@@ -301,9 +323,17 @@ __global__ void __launch_bounds__(512, (LSTM_W4 && MT == 1) ? 4 : 2) bilstm_h3_k
         for (int r = 0; r < 16; ++r) acc[mt][g][r] = bv;
     }
     if constexpr (W4 && LSTM_W4 == 2) {
-      // one gate ahead: the next (k-step, gate)'s B fragments in flight under this gate's MFMAs
-      f16x8 gh = *reinterpret_cast<const f16x8*>(wh0);
-      f16x8 gl = *reinterpret_cast<const f16x8*>(wl0);
+      // one gate ahead: the next (k-step, gate)'s B fragments in flight under this gate's MFMAs.
+      // Addressed as a uniform (SGPR) base + this lane's 32-bit byte offset, so every load is one
+      // global_load with saddr and no per-load 64-bit address arithmetic
+      const uint32_t lob = (uint32_t)(wave * KST * 512 + lane * 8) * 2u;
+      const __amdgpu_buffer_rsrc_t rh = lstm_rsrc(Wh, (uint32_t)(4 * GS * 2));
+      const __amdgpu_buffer_rsrc_t rl = lstm_rsrc(Wl, (uint32_t)(4 * GS * 2));
+      auto frag = [&](__amdgpu_buffer_rsrc_t r, size_t uoff) {
+        return __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(r, lob, (int)(uoff * 2), 0));
+      };
+      f16x8 gh = frag(rh, 0);
+      f16x8 gl = frag(rl, 0);
 #pragma unroll 1
       for (int ks = 0; ks < KST; ++ks) {
         const f16x8 ah = *reinterpret_cast<const f16x8*>(arow_h + 16 * ks);
@@ -311,8 +341,8 @@ __global__ void __launch_bounds__(512, (LSTM_W4 && MT == 1) ? 4 : 2) bilstm_h3_k
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const int gn = g < 3 ? g + 1 : 0, kn = g < 3 ? ks : (ks + 1 < KST ? ks + 1 : ks);
-          const f16x8 nh = *reinterpret_cast<const f16x8*>(wh0 + gn * GS + 512 * kn);
-          const f16x8 nl = *reinterpret_cast<const f16x8*>(wl0 + gn * GS + 512 * kn);
+          const f16x8 nh = frag(rh, gn * GS + 512 * (size_t)kn);
+          const f16x8 nl = frag(rl, gn * GS + 512 * (size_t)kn);
           acc[0][g] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, gh, acc[0][g], 0, 0, 0);
           acc[0][g] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, gl, acc[0][g], 0, 0, 0);
           acc[0][g] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, gh, acc[0][g], 0, 0, 0);
