@@ -134,6 +134,8 @@ struct mmla_ctx {
   // ... and the last one with the final BN + ReLU + AvgPool4 (siu.hip FIN); env MMLA_NO_SIFIN=1: the
   // unit writes its output and bn_relu_avgpool4 runs as its own launch
   bool sifin = true;
+  // fused SI pipeline: si_fe writes 40-float feature rows for the stem (env MMLA_NO_SIPAD=1: 39)
+  bool si_pad_feat = true;
   // 3xFP16 range guard: kernels set range_dev[0] (device-pointer calls; sticky until
   // mmla_range_check) or range_dev[1] (host-pointer micro-batches: re-run in exact f32) when an
   // operand they split into fp16 is >= 65504 in magnitude or not finite
@@ -882,8 +884,10 @@ int run_od_net(mmla_ctx* c, const uint8_t* img_u8, const float* img_f32, int64_t
   return MMLA_OK;
 }
 
+// ldx: the features' row stride (39, or 40 from si_fe with a zero 40th column: the stem then stages
+// 16-B aligned rows, conv_h3's float4 path, bit-identical -- its weights' padded channels are zero)
 int run_si_net(mmla_ctx* c, const float* x, int64_t n, float* probs, int32_t* argmax,
-               const uint8_t* silent) {
+               const uint8_t* silent, int ldx = SI_D) {
   const SiNet& W = c->si;
   const size_t big = (size_t)n * SI_T * 32 * sizeof(float);
   void *px, *pt1, *pt2, *pt3, *pseq, *ph, *pl;
@@ -901,7 +905,10 @@ int run_si_net(mmla_ctx* c, const float* x, int64_t n, float* probs, int32_t* ar
   int t = SI_T;
   bool fused_final = false;   // the last unit wrote BN + ReLU + AvgPool4 itself (siu FIN)
   // Conv1D(32, 4, same): [n, 256, 1, 39] -> [n, 256, 1, 32] (speaker_identification.py:195)
-  CHK(conv_spatial(c, W.stem, x, X, (int)n, t, 1, nullptr, PRO_NONE, EPI_BIAS, nullptr));
+  ConvW stem = W.stem;
+  if (ldx == SI_D + 1 && c->precision == MMLA_PREC_F16X3 && stem.wh && stem.cin_pad > SI_D) stem.cin = ldx;
+  else if (ldx != SI_D) return fail(c, MMLA_E_INVALID, "padded SI features need the 3xFP16 stem");
+  CHK(conv_spatial(c, stem, x, X, (int)n, t, 1, nullptr, PRO_NONE, EPI_BIAS, nullptr));
   for (int u = 0; u < 9; ++u) {   // res_unit, speaker_identification.py:168-190
     const SiUnit& U = W.unit[u];
     const int cin = U.ca.cin;
@@ -1082,6 +1089,7 @@ int mmla_create(int device, mmla_ctx** out) {
   if (const char* su = std::getenv("MMLA_NO_SIU")) c->siu = std::atoi(su) == 0;
   if (const char* sp = std::getenv("MMLA_NO_SIPU")) c->sipu = std::atoi(sp) == 0;
   if (const char* sf = std::getenv("MMLA_NO_SIFIN")) c->sifin = std::atoi(sf) == 0;
+  if (const char* sd = std::getenv("MMLA_NO_SIPAD")) c->si_pad_feat = std::atoi(sd) == 0;
   // a BLOCKING stream: it orders with the legacy default (NULL) stream, on which PyTorch's default
   // stream enqueues -- so a device-pointer call sees tensors a torch kernel or copy just produced
   // without an explicit synchronisation (a non-blocking stream raced them: a 65 536-clip call read
@@ -1659,7 +1667,10 @@ int mmla_si_pipeline(mmla_ctx* c, const int16_t* pcm, int64_t n, int64_t stride,
       Pcm p;
       CHK(stage_pcm(c, pcm, c0, cnt, stride, lens, clip_len, SI_NEED_SAMPLES, dev, &p));
       void *pf, *ps;
-      CHK(ws_get(c, S_FEAT, cnt * SI_T * SI_D * sizeof(float), &pf));
+      // the features stay on the device: rows of 40 floats when the 3xFP16 stem reads them
+      const int ldf = c->precision == MMLA_PREC_F16X3 && c->si.stem.wh && c->si.stem.cin_pad > SI_D &&
+                              c->si_pad_feat ? SI_D + 1 : SI_D;
+      CHK(ws_get(c, S_FEAT, cnt * SI_T * ldf * sizeof(float), &pf));
       CHK(ws_get(c, S_SILENT, cnt, &ps));
       SiFeArgs a{};
       a.pcm = p.p;
@@ -1668,13 +1679,14 @@ int mmla_si_pipeline(mmla_ctx* c, const int16_t* pcm, int64_t n, int64_t stride,
       a.clip_len = lens ? 0 : clip_len;
       a.tables = c->si_tables;
       a.feat = static_cast<float*>(pf);
+      a.ldf = ldf;
       a.silent = static_cast<uint8_t*>(ps);
       LAUNCH(c, MMLA_STAGE_SI_FE, si_fe_bytes(cnt, a), si_fe_launch(a, cnt, c->stream));
       float* dp;
       int32_t* da;
       CHK(out_ptr(c, probs, c0 * k, cnt * k, dev, S_OUT0, &dp));
       CHK(out_ptr(c, argmax, c0, cnt, dev, S_OUT1, &da));
-      CHK(run_si_net(c, a.feat, cnt, dp, da, a.silent));
+      CHK(run_si_net(c, a.feat, cnt, dp, da, a.silent, ldf));
       CHK(copy_back(c, probs, c0 * k, dp, cnt * k, dev));
       CHK(copy_back(c, argmax, c0, da, cnt, dev));
       if (silent) {

@@ -881,6 +881,8 @@ hipError_t conv_h3_launch(ConvH3Args a, hipStream_t s) {
   H3(3, 1, 32, 1, PRO_BN_RELU, EPI_BIAS, false)
   H3(3, 1, 32, 1, PRO_BN_RELU, EPI_ADD, false)
   H3(3, 1, 32, 1, PRO_BN_RELU, EPI_ADD_SC, false)
+  // SI stem Conv1D(32, 4) on 40-float feature rows (si_fe's padded layout; speaker_identification.py:195)
+  H3(4, 1, 16, 1, PRO_NONE, EPI_BIAS, false)
   // SI-NET Dense head as a 1x1 conv over the clips (speaker_identification.py:216)
   H3(1, 1, 32, 1, PRO_NONE, EPI_BIAS, false)
 #undef H3

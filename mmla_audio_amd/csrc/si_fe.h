@@ -29,7 +29,8 @@ struct SiFeArgs {
   int32_t clip_len;
   int64_t seq_len;          // > 0: sequence mode -- block s = 256-frame window s of one signal
   const SiFeTables* tables;
-  float* feat;              // [n,256,39]
+  float* feat;              // [n,256,ldf]
+  int ldf;                  // feature row stride: 39 (0 = 39), or 40 with a zero 40th column
   uint8_t* silent;          // [n] nullable (clip mode only)
 };
 

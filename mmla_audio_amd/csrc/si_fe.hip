@@ -148,7 +148,10 @@ __global__ void __launch_bounds__(NT, SI_MINB) si_fe_kernel(SiFeArgs a) {
   const SiFeTables& tb = *a.tables;
   const int lane = threadIdx.x;
   const int64_t blk = blockIdx.x;
-  float* out = a.feat + blk * (OUTF * 39);
+  // feature rows of ldf floats: 39, or 40 with a zero 40th column (the fused SI pipeline: the stem
+  // Conv1D then stages 16-B aligned rows as float4, conv_h3 V4)
+  const int ldf = a.ldf > 39 ? 40 : 39;
+  float* out = a.feat + blk * (OUTF * ldf);
 
   const int16_t* x;
   int64_t len, frame0;
@@ -162,7 +165,7 @@ __global__ void __launch_bounds__(NT, SI_MINB) si_fe_kernel(SiFeArgs a) {
     frame0 = 0;
     if (len < 4000) {             // speaker_identification.py:375-376
       float4* o4 = reinterpret_cast<float4*>(out);
-      for (int e = lane; e < OUTF * 39 / 4; e += NT) o4[e] = float4{0.f, 0.f, 0.f, 0.f};
+      for (int e = lane; e < OUTF * ldf / 4; e += NT) o4[e] = float4{0.f, 0.f, 0.f, 0.f};
       if (a.silent && lane == 0) a.silent[blk] = 1;
       return;
     }
@@ -394,7 +397,7 @@ __global__ void __launch_bounds__(NT, SI_MINB) si_fe_kernel(SiFeArgs a) {
       const int64_t g = g0 + dcf;
       if (g < g_hi) {
         const int lf = (int)(g - lbase);
-        if (lf >= HALO && lf < HALO + OUTF) out[(lf - HALO) * 39 + dcc] = (float)v;
+        if (lf >= HALO && lf < HALO + OUTF) out[(lf - HALO) * ldf + dcc] = (float)v;
         else sm.ext[lf < HALO ? lf : lf - OUTF][dcc] = (float)v;
       }
     }
@@ -413,7 +416,7 @@ __global__ void __launch_bounds__(NT, SI_MINB) si_fe_kernel(SiFeArgs a) {
       const int lf = e / 13, c = e - lf * 13;
       const int64_t g = lbase + lf;
       if (g >= g_lo && g < g_hi)
-        C[e] = (lf >= HALO && lf < HALO + OUTF) ? out[(lf - HALO) * 39 + c]
+        C[e] = (lf >= HALO && lf < HALO + OUTF) ? out[(lf - HALO) * ldf + c]
                                                 : sm.ext[lf < HALO ? lf : lf - OUTF][c];
     }
   }
@@ -434,7 +437,8 @@ __global__ void __launch_bounds__(NT, SI_MINB) si_fe_kernel(SiFeArgs a) {
     const int e = lane + NT * i;
     const int t = e / 13, c = e - t * 13;
     const int64_t g = frame0 + t;
-    float* o = out + t * 39 + c;
+    float* o = out + t * ldf + c;
+    if (ldf == 40 && c == 12) o[27] = 0.0f;   // the pad column 39 (t * 40 + 39)
     float v0 = 0.0f, v1 = 0.0f, v2 = 0.0f;
     if (g < T) {
       v0 = C[(t + HALO) * 13 + c];
