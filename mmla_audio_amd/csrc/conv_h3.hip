@@ -56,6 +56,30 @@ constexpr float ACT_SCALE = 16.0f;      // 2^4: staged activations
 // weights are split at a per-tensor power-of-two scale (conv_h3_split_weights, capi.cpp pick_wscale:
 // 2^8 for the usual |w| in [1/16, 255.9)); the epilogue multiplies by a.unscale = 2^-4 / that scale
 constexpr float ACT_RANGE = 65504.0f / ACT_SCALE;   // largest finite fp16 / the activation scale
+// CONV_H3_BUFB: the B fragments by raw buffer loads from a wave-uniform descriptor (voffset = the
+// lane's 32-bit offset, soffset = the uniform (tap, k-step) offset): no per-load 64-bit address VALU
+#ifndef CONV_H3_BUFB
+#define CONV_H3_BUFB 1
+#endif
+MMLA_DEV __amdgpu_buffer_rsrc_t h3_rsrc(const void* p) {
+  const uint64_t u = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)u);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(u >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), (short)0,
+                                           (int)0x7fffffff, 0x00020000);
+}
+// 16 B of a split weight at half index uoff (wave-uniform) + lofs (this lane's)
+MMLA_DEV f16x8 h3_frag(const uint16_t* base, __amdgpu_buffer_rsrc_t r, size_t uoff, int lofs) {
+#if CONV_H3_BUFB
+  (void)base;
+  return __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(r, (uint32_t)lofs * 2u,
+                                                                         (int)(uoff * 2), 0));
+#else
+  (void)r;
+  return *reinterpret_cast<const f16x8*>(base + uoff + lofs);
+#endif
+}
+
 
 template <int PRO>
 MMLA_DEV float pro_fn(float v, float sc, float sh) {
@@ -262,6 +286,7 @@ __global__ void __launch_bounds__(NT, (conv_minw<KH, BN, TW, EPI, SHP::FIXED>())
   int lofs[NTL];
 #pragma unroll
   for (int nt = 0; nt < NTL; ++nt) lofs[nt] = (n0 / 32 + wn * NTL + nt) * 512 + lane * 8;
+  const __amdgpu_buffer_rsrc_t rwh = h3_rsrc(a.wh), rwl = h3_rsrc(a.wl);
   const size_t tap_stride = (size_t)A_COUTP * A_CINP;
   const size_t kstride = (size_t)(A_COUTP / 32) * 512;   // one 16-channel k-step
   // the epilogue's bias, loaded now: after the MFMA loop it cost a memory round trip of its own
@@ -340,8 +365,8 @@ __global__ void __launch_bounds__(NT, (conv_minw<KH, BN, TW, EPI, SHP::FIXED>())
 #pragma unroll
         for (int s = 0; s < KS; ++s) {
           const size_t u = (size_t)(ch * KS + s) * kstride;
-          bh[nt][s] = *reinterpret_cast<const f16x8*>(a.wh + u + lofs[nt]);
-          bl[nt][s] = *reinterpret_cast<const f16x8*>(a.wl + u + lofs[nt]);
+          bh[nt][s] = h3_frag(a.wh, rwh, u, lofs[nt]);
+          bl[nt][s] = h3_frag(a.wl, rwl, u, lofs[nt]);
         }
     };
     if constexpr (EARLY_B) load_b0();
@@ -419,8 +444,8 @@ __global__ void __launch_bounds__(NT, (conv_minw<KH, BN, TW, EPI, SHP::FIXED>())
 #pragma unroll
           for (int s = 0; s < KS; ++s) {
             const size_t u = (tap + 1) * tap_stride + (size_t)(ch * KS + s) * kstride;
-            nbh[nt][s] = *reinterpret_cast<const f16x8*>(a.wh + u + lofs[nt]);
-            nbl[nt][s] = *reinterpret_cast<const f16x8*>(a.wl + u + lofs[nt]);
+            nbh[nt][s] = h3_frag(a.wh, rwh, u, lofs[nt]);
+            nbl[nt][s] = h3_frag(a.wl, rwl, u, lofs[nt]);
           }
       }
 #pragma unroll
@@ -611,8 +636,8 @@ __global__ void __launch_bounds__(NT, (conv_minw<KH, BN, TW, EPI, SHP::FIXED>())
         f16x8 bh_[NTL], bl_[NTL];
 #pragma unroll
         for (int nt = 0; nt < NTL; ++nt) {
-          bh_[nt] = *reinterpret_cast<const f16x8*>(a.sc_wh + (size_t)s * sks + lofs[nt]);
-          bl_[nt] = *reinterpret_cast<const f16x8*>(a.sc_wl + (size_t)s * sks + lofs[nt]);
+          bh_[nt] = h3_frag(a.sc_wh, h3_rsrc(a.sc_wh), (size_t)s * sks, lofs[nt]);
+          bl_[nt] = h3_frag(a.sc_wl, h3_rsrc(a.sc_wl), (size_t)s * sks, lofs[nt]);
         }
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {

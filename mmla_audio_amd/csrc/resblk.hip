@@ -85,6 +85,31 @@ __device__ __forceinline__ void split2(f32x2 v, f16x2& h, f16x2& l) {
   l = __builtin_convertvector(v - hf, f16x2);
 }
 
+// RB_BUFB: GEMM 1 / GEMM 2 B fragments by raw buffer loads from a wave-uniform descriptor
+// (voffset = the lane's offset, soffset = the uniform (k-step, tile) offset): no per-load 64-bit
+// address VALU (as conv_h3.hip CONV_H3_BUFB)
+#ifndef RB_BUFB
+#define RB_BUFB 1
+#endif
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rb_rsrc(const void* p) {
+  const uint64_t u = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)u);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(u >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), (short)0,
+                                           (int)0x7fffffff, 0x00020000);
+}
+// 16 B of a split weight at half index uoff (wave-uniform) + lofs (this lane's)
+__device__ __forceinline__ f16x8 rb_frag(const uint16_t* base, __amdgpu_buffer_rsrc_t r, int uoff,
+                                         int lofs) {
+#if RB_BUFB
+  (void)base;
+  return __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(r, (uint32_t)lofs * 2u, uoff * 2, 0));
+#else
+  (void)r;
+  return *reinterpret_cast<const f16x8*>(base + uoff + lofs);
+#endif
+}
+
 // the 3 channels of image pixel `pix` (uint8 decoded PNG or float NHWC), as floats
 // 3xFP16 range guard: false when a value about to be split leaves the fp16 range once scaled
 // (|v| >= 65504 / 2^4) or is not finite
@@ -302,13 +327,14 @@ __global__ void __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(R
   // 16 rows at 64 B each)
   const int b1o = (wn * NTW) * 512 + lane * 8;   // + nt * 512 + s * B1KS
   constexpr int B1KS = (C / 16) * 512;
+  const __amdgpu_buffer_rsrc_t rw1h = rb_rsrc(a.w1h), rw1l = rb_rsrc(a.w1l);
   f16x8 bh[PF][NTW], bl[PF][NTW];   // ring of B fragments, PF k-steps ahead
 #pragma unroll
   for (int s = 0; s < PF && s < KS1; ++s)
 #pragma unroll
     for (int nt = 0; nt < NTW; ++nt) {
-      bh[s][nt] = *reinterpret_cast<const f16x8*>(a.w1h + b1o + nt * 512 + B1KS * s);
-      bl[s][nt] = *reinterpret_cast<const f16x8*>(a.w1l + b1o + nt * 512 + B1KS * s);
+      bh[s][nt] = rb_frag(a.w1h, rw1h, nt * 512 + B1KS * s, b1o);
+      bl[s][nt] = rb_frag(a.w1l, rw1l, nt * 512 + B1KS * s, b1o);
     }
 
   if constexpr (STEM) {
@@ -448,8 +474,8 @@ __global__ void __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(R
       if (s + PF < KS1) {
 #pragma unroll
         for (int nt = 0; nt < NTW; ++nt) {
-          bh[s % PF][nt] = *reinterpret_cast<const f16x8*>(a.w1h + b1o + nt * 512 + B1KS * (s + PF));
-          bl[s % PF][nt] = *reinterpret_cast<const f16x8*>(a.w1l + b1o + nt * 512 + B1KS * (s + PF));
+          bh[s % PF][nt] = rb_frag(a.w1h, rw1h, nt * 512 + B1KS * (s + PF), b1o);
+          bl[s % PF][nt] = rb_frag(a.w1l, rw1l, nt * 512 + B1KS * (s + PF), b1o);
         }
       }
 #pragma unroll
@@ -529,12 +555,13 @@ __global__ void __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(R
     const int b2o = ((wn * NTW) * 16 + col) * G::LW2 + 8 * grp;
     // !W2LDS: GEMM 2's B from L2 in fragment order (resblk_split_weights, frag), one k-step ahead
     const int b2g = (wn * NTW) * 512 + lane * 8;   // + nt * 512 + s * (C / 16) * 512
+    const __amdgpu_buffer_rsrc_t rw2h = rb_rsrc(a.w2h), rw2l = rb_rsrc(a.w2l);
     f16x8 ph[NTW], pl[NTW];
     if constexpr (!G::W2LDS) {
 #pragma unroll
       for (int nt = 0; nt < NTW; ++nt) {
-        ph[nt] = *reinterpret_cast<const f16x8*>(a.w2h + b2g + nt * 512);
-        pl[nt] = *reinterpret_cast<const f16x8*>(a.w2l + b2g + nt * 512);
+        ph[nt] = rb_frag(a.w2h, rw2h, nt * 512, b2g);
+        pl[nt] = rb_frag(a.w2l, rw2l, nt * 512, b2g);
       }
     }
 #pragma unroll
@@ -552,8 +579,8 @@ __global__ void __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(R
           gh[nt] = ph[nt];
           gl[nt] = pl[nt];
           if (s + 1 < KS2) {
-            ph[nt] = *reinterpret_cast<const f16x8*>(a.w2h + b2g + nt * 512 + (s + 1) * (C / 16) * 512);
-            pl[nt] = *reinterpret_cast<const f16x8*>(a.w2l + b2g + nt * 512 + (s + 1) * (C / 16) * 512);
+            ph[nt] = rb_frag(a.w2h, rw2h, nt * 512 + (s + 1) * (C / 16) * 512, b2g);
+            pl[nt] = rb_frag(a.w2l, rw2l, nt * 512 + (s + 1) * (C / 16) * 512, b2g);
           }
         }
       }
