@@ -37,6 +37,17 @@
 #include "si_fe.h"
 
 #include <cstdlib>
+#include <type_traits>
+
+// SI_F32FB 1: the power spectrum is stored and the filterbank summed in float32 after the float64
+// FFT and real split (which must stay float64: a tone near Nyquist makes the weak low bins the
+// difference of two huge values); the sums of positive powers are well conditioned, the features
+// move by <= ~3e-6 from the float64 oracle (numpy model on the worst-case tones) against the 1e-4
+// bar.  The float64 sub-segment sums had cost 13 % of the kernel (a build without them: 26.6 ->
+// 23.2 ms per 3 SI steps)
+#ifndef SI_F32FB
+#define SI_F32FB 1
+#endif
 
 namespace {
 
@@ -66,6 +77,10 @@ constexpr int WIN = 888;                        // samples [160 g0 - 8, 160 g0 +
 constexpr int WCH = WIN / 8;                    // 111 16-B chunks
 constexpr int FP = 273;                         // frame region pitch (cd): 16 pass-A rows of 17 + 1
 constexpr int PART = 258;                       // region doubles: P[0..256], then (A, B) sub sums
+// the power spectrum / sub-sum element type (SI_F32FB) and the sub sums' offset in that type
+typedef std::conditional<SI_F32FB != 0, float, double>::type fbt;
+typedef std::conditional<SI_F32FB != 0, float2, double2>::type fbt2;
+constexpr int PSUM = SI_F32FB ? 2 * PART : PART;   // same byte offset either way
 constexpr int LFE = PART + 2 * SI_FE_MAX_SUB;   // then 27 log energies
 static_assert(LFE + 27 <= 2 * FP, "frame region");
 static_assert(NL * 13 * sizeof(float) <= R * FP * sizeof(cd), "epilogue cepstra tile");
@@ -126,6 +141,9 @@ MMLA_DEV void split_power(cd z, cd zr, cd w, double& pk, double& pnk) {
 // ocml's log (~1e-16) is a ~40-instruction routine run 27 times per frame.  The features' tolerance
 // is 1e-4 absolute after the DCT (|coefficient| <= 0.28 over 26 logs) and the lifter (<= 12):
 // the bound stays below 2e-5 even if every term's error had the same sign
+#ifndef SI_EXP
+#define SI_EXP 0   // dev timing bounds (garbage outputs): 1 = no sub-segment sums, 2 = no split either
+#endif
 #ifndef SI_FAST_LOG
 #define SI_FAST_LOG 1
 #endif
@@ -312,42 +330,42 @@ __global__ void __launch_bounds__(NT, SI_MINB) si_fe_kernel(SiFeArgs a) {
         for (int q2 = 0; q2 < 4; ++q2) sm.z[fq][q + 16 * (q1 + 4 * q2)] = v[4 * q1 + q2];
     }
     lds_order();
-    // ---- split: P[k] for k = lane, 256 - lane, lane + 64, 192 - lane (+ 128), doubles over Z ------
+    // ---- split: P[k] for k = lane, 256 - lane, lane + 64, 192 - lane (+ 128), fbt over Z ----------
 #pragma unroll
-    for (int f = 0; f < R; ++f) {
+    for (int f = 0; f < (SI_EXP >= 2 ? 0 : R); ++f) {
       const cd* Z = sm.z[f];
-      double* P = reinterpret_cast<double*>(sm.z[f]);
+      fbt* P = reinterpret_cast<fbt*>(sm.z[f]);
       const cd za = Z[lane], zar = Z[(256 - lane) & 255], zb = Z[lane + 64], zbr = Z[192 - lane];
       const cd zm = Z[128];
       lds_order();
       double p0, p1, p2, p3;
       split_power(za, zar, wa, p0, p1);
       split_power(zb, zbr, wb, p2, p3);
-      P[lane] = p0;
-      P[256 - lane] = p1;
-      P[lane + 64] = p2;
-      P[192 - lane] = p3;
-      if (lane == 0) P[128] = (zm.x * zm.x + zm.y * zm.y) * (1.0 / 512.0);
+      P[lane] = (fbt)p0;
+      P[256 - lane] = (fbt)p1;
+      P[lane + 64] = (fbt)p2;
+      P[192 - lane] = (fbt)p3;
+      if (lane == 0) P[128] = (fbt)((zm.x * zm.x + zm.y * zm.y) * (1.0 / 512.0));
     }
     lds_order();
     // ---- sub-segment sums: A = sum P[k], B = sum (k - bin[s]) P[k] = sum i P + d0 A -------------------
 #pragma unroll
-    for (int s = 0; s < 3; ++s) {
+    for (int s = 0; s < (SI_EXP >= 1 ? 0 : 3); ++s) {
       const int scn = (stask[s] >> 9) & 15;
       if (scn > 0) {
-        double* Q = reinterpret_cast<double*>(sm.z[(stask[s] >> 13) & 3]);
-        const double* p = Q + (stask[s] & 511);
-        double A = 0.0, B = 0.0;
+        fbt* Q = reinterpret_cast<fbt*>(sm.z[(stask[s] >> 13) & 3]);
+        const fbt* p = Q + (stask[s] & 511);
+        fbt A = 0, B = 0;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-          const double v = p[i];                 // past the sub-segment: finite LDS words, not used
-          const double pv = i < scn ? v : 0.0;
+          const fbt v = p[i];                    // past the sub-segment: finite LDS words, not used
+          const fbt pv = i < scn ? v : (fbt)0;
           A += pv;
-          if (i > 0) B = fma((double)i, pv, B);
+          if (i > 0) B = fma((fbt)i, pv, B);
         }
         int d0 = (stask[s] >> 21) & 511;
         asm volatile("" : "+v"(d0));   // converted here: a hoisted double of it was spilled
-        reinterpret_cast<double2*>(Q + PART)[(stask[s] >> 15) & 63] = double2{A, fma((double)d0, A, B)};
+        reinterpret_cast<fbt2*>(Q + PSUM)[(stask[s] >> 15) & 63] = fbt2{A, fma((fbt)d0, A, B)};
       }
     }
     lds_order();
@@ -356,30 +374,30 @@ __global__ void __launch_bounds__(NT, SI_MINB) si_fe_kernel(SiFeArgs a) {
     for (int s = 0; s < 2; ++s) {
       if (lane < 52 || (s == 0 && lane < 56)) {
         const int f = lane < 52 ? 2 * s + lane / 26 : lane - 52;
-        double* Q = reinterpret_cast<double*>(sm.z[f]);
-        const double2* ps = reinterpret_cast<const double2*>(Q + PART);
+        const fbt* Q = reinterpret_cast<const fbt*>(sm.z[f]);
+        const fbt2* ps = reinterpret_cast<const fbt2*>(Q + PSUM);
         double arg;
         int slot;
         if (lane < 52) {
-          double bj = 0.0, aj1 = 0.0, bj1 = 0.0;
+          fbt bj = 0, aj1 = 0, bj1 = 0;
 #pragma unroll
           for (int i = 0; i < 4; ++i)
             if (u0 + i < u1) bj += ps[u0 + i].y;
 #pragma unroll
           for (int i = 0; i < 4; ++i)
             if (u1 + i < u2) {
-              const double2 v = ps[u1 + i];
+              const fbt2 v = ps[u1 + i];
               aj1 += v.x;
               bj1 += v.y;
             }
-          arg = fma(bj, iw0, aj1 - bj1 * iw1);
+          arg = (double)fma(bj, (fbt)iw0, aj1 - bj1 * (fbt)iw1);
           slot = fj;
         } else {
-          arg = 0.5 * (sm.s2[f] + Q[0] + Q[256]);   // Parseval: sum_{k=0}^{256} P[k]
+          arg = 0.5 * (sm.s2[f] + (double)Q[0] + (double)Q[256]);   // Parseval: sum_{k=0}^{256} P[k]
           slot = 26;
         }
         if (arg == 0.0) arg = 2.220446049250313e-16;   // numpy.finfo(float).eps
-        Q[LFE + slot] = log_pos(arg);
+        reinterpret_cast<double*>(sm.z[f])[LFE + slot] = log_pos(arg);
       }
     }
     lds_order();
