@@ -127,13 +127,15 @@ MMLA_DEV void dft16(cd v[16]) {
 }
 
 // P[k] and P[256 - k] (|X|^2 / 512) of the 512-point real DFT from Z[k], Z[256 - k]
+// (computed at twice the scale: the halvings of e and o and the 1/512 fold into one 1/2048 -- powers
+// of two, so every rounding is the same and the result bit-identical, four multiplies fewer)
 MMLA_DEV void split_power(cd z, cd zr, cd w, double& pk, double& pnk) {
-  const cd e = {0.5 * (z.x + zr.x), 0.5 * (z.y - zr.y)};   // (Z[k] + conj Z[-k]) / 2
-  const cd o = {0.5 * (z.y + zr.y), -0.5 * (z.x - zr.x)};  // (Z[k] - conj Z[-k]) / 2i
+  const cd e = {z.x + zr.x, z.y - zr.y};                   // Z[k] + conj Z[-k]
+  const cd o = {z.y + zr.y, zr.x - z.x};                   // (Z[k] - conj Z[-k]) / i
   const cd wo = cmul(w, o);
-  const cd xp = cadd(e, wo), xm = csub(e, wo);             // X[k], conj X[256 - k]
-  pk = (xp.x * xp.x + xp.y * xp.y) * (1.0 / 512.0);
-  pnk = (xm.x * xm.x + xm.y * xm.y) * (1.0 / 512.0);
+  const cd xp = cadd(e, wo), xm = csub(e, wo);             // 2 X[k], 2 conj X[256 - k]
+  pk = (xp.x * xp.x + xp.y * xp.y) * (1.0 / 2048.0);
+  pnk = (xm.x * xm.x + xm.y * xm.y) * (1.0 / 2048.0);
 }
 
 // natural log of a positive finite double (the filterbank energies): exponent from frexp, log2 of the
