@@ -37,6 +37,28 @@ __global__ void od_stem_kernel(const T* __restrict__ x, int64_t n_pix, const flo
   reinterpret_cast<float4*>(y)[i] = o;
 }
 
+// float4 over channels (c % 4 == 0): the same per-channel summation order, a quarter of the loads
+__global__ void mean_h4_kernel(const float4* __restrict__ x, int n, int h, int w, int c4,
+                               float4* __restrict__ y) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;   // over n*w*c4
+  const int64_t tot = (int64_t)n * w * c4;
+  if (i >= tot) return;
+  const int ci = (int)(i % c4);
+  const int64_t r = i / c4;
+  const int wi = (int)(r % w);
+  const int64_t ni = r / w;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int hh = 0; hh < h; ++hh) {
+    const float4 v = x[((ni * h + hh) * w + wi) * c4 + ci];
+    s.x += v.x;
+    s.y += v.y;
+    s.z += v.z;
+    s.w += v.w;
+  }
+  const float fh = (float)h;
+  y[i] = make_float4(s.x / fh, s.y / fh, s.z / fh, s.w / fh);
+}
+
 __global__ void mean_h_kernel(const float* __restrict__ x, int n, int h, int w, int c,
                               float* __restrict__ y) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;   // over n*w*c
@@ -527,6 +549,11 @@ hipError_t od_stem_launch(const uint8_t* img_u8, const float* img_f32, int64_t n
 hipError_t mean_h_launch(const float* x, int n, int h, int w, int c, float* y, hipStream_t s) {
   const int64_t tot = (int64_t)n * w * c;
   if (tot <= 0) return hipSuccess;
+  if (c % 4 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0 && (reinterpret_cast<uintptr_t>(y) & 15) == 0) {
+    hipLaunchKernelGGL(mean_h4_kernel, dim3(blocks_for(tot / 4, 256)), dim3(256), 0, s,
+                       reinterpret_cast<const float4*>(x), n, h, w, c / 4, reinterpret_cast<float4*>(y));
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(mean_h_kernel, dim3(blocks_for(tot, 256)), dim3(256), 0, s, x, n, h, w, c, y);
   return hipGetLastError();
 }
