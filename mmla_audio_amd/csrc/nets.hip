@@ -194,6 +194,9 @@ __global__ void __launch_bounds__(256) bilstm_kernel(const float* __restrict__ s
 
 
 // ---- 3xFP16 BiLSTM ----------------------------------------------------------------------------
+// (Round 4: 32 clips per workgroup at two workgroups per CU, or 64 clips at one per CU for batches
+// >= LSTM_MT2_MIN; B by buffer loads one gate ahead; gate reciprocals on v_rcp_f32 -- see LSTM_W4,
+// LSTM_RCP and bilstm_h3_launch.)
 // The same recurrence with the [32 x 384] x [384 x 1024] step product on the f16 MFMA
 // (v_mfma_f32_32x32x16_f16) with 3xFP16 products: A = [h_{t-1} | x_t] split into fp16 hi/lo in LDS,
 // B = the stacked kernels pre-split on the host and packed in MFMA fragment order (a lane's 8
