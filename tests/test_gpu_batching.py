@@ -102,3 +102,20 @@ def test_oom_retry_halves_this_call_only(monkeypatch):
     assert c.get_microbatch()[0] == mb0  # not capped at 75 for later calls
     p2, _, _ = c.od_pipeline(pcm)
     assert np.array_equal(p2, p_ref)
+
+
+def test_large_batches_match_batch_one(ctx):
+    """Batches of >= 8192 clips run the BiLSTM with 64-clip workgroups (nets.hip LSTM_MT2_MIN), small
+    ones with 32-clip workgroups: the same clip must give the same bits either way (OD and SI)."""
+    base_od = synth.batch(1700, 24, 40000)
+    pcm = np.tile(base_od, (342, 1))[:8200]          # 8200 clips, 24 distinct
+    p_all, a_all, _ = ctx.od_pipeline(pcm)
+    for i in (0, 4111, 8199):
+        p1, a1, _ = ctx.od_pipeline(pcm[i:i + 1])
+        assert np.array_equal(p1[0], p_all[i]) and a1[0] == a_all[i]
+    base_si = synth.batch(1800, 24, 24000)
+    pcm = np.tile(base_si, (342, 1))[:8200]
+    p_all, a_all, _ = ctx.si_pipeline(pcm)
+    for i in (1, 4100, 8198):
+        p1, a1, _ = ctx.si_pipeline(pcm[i:i + 1])
+        assert np.array_equal(p1[0], p_all[i]) and a1[0] == a_all[i]
