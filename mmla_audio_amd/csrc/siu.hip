@@ -224,6 +224,23 @@ __global__ void __launch_bounds__(64 * NW, 2) siu_kernel(SiuArgs a) {
   }
   __syncthreads();
   // ---- GEMM b: output rows r0 + m, m < R (t1 LDS row of output row m at tap dy: m + dy) -----------
+  // EARLY: the residuals of all MT tiles loaded before GEMM b, so their latency hides under it
+  // (units without pooling whose registers allow it: MT 2)
+#ifndef SIU_EARLY_RSD
+#define SIU_EARLY_RSD 1
+#endif
+  constexpr bool EARLY = SIU_EARLY_RSD && !POOL && MT <= 2;
+  float ersd[EARLY ? MT : 1][16];
+  if constexpr (EARLY) {
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = (wm * MT + mt) * 32 + (r & 3) + 8 * (r >> 2) + hsel;
+        const int64_t g = r0 + m;
+        ersd[mt][r] = m < R && g < HH ? a.x[g * C + co] : 0.0f;
+      }
+  }
   gemm(std::integral_constant<int, NCH>{}, std::integral_constant<int, LDP>{}, a.wbh, a.wbl, r0, acc);
   {
     const float b = a.bb[co];
@@ -272,7 +289,7 @@ __global__ void __launch_bounds__(64 * NW, 2) siu_kernel(SiuArgs a) {
         for (int r = 0; r < 16; ++r) {
           const int m = (wm * MT + mt) * 32 + (r & 3) + 8 * (r >> 2) + hsel;
           const int64_t g = r0 + m;
-          rsd[r] = m < R && g < HH ? a.x[g * C + co] : 0.0f;
+          rsd[r] = EARLY ? ersd[EARLY ? mt : 0][r] : (m < R && g < HH ? a.x[g * C + co] : 0.0f);
         }
       }
       if constexpr (FIN) {
