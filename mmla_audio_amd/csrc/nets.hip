@@ -502,24 +502,46 @@ __global__ void si_head_kernel(const float* __restrict__ logits, int n, int k, i
   const int64_t clip = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   if (clip >= n) return;
   const float* z = logits + clip * ld;
+  // the logits are read once (K <= 64 KREG: registers; larger K: re-read), each exponential taken once
+  constexpr int KREG = 16;
+  float zr[KREG];
   float m = -INFINITY;
-  for (int i = lane; i < k; i += 64) m = fmaxf(m, z[i]);
+#pragma unroll
+  for (int j = 0; j < KREG; ++j) {
+    const int i = lane + 64 * j;
+    zr[j] = i < k ? z[i] : -INFINITY;
+    m = fmaxf(m, zr[j]);
+  }
+  for (int i = lane + 64 * KREG; i < k; i += 64) m = fmaxf(m, z[i]);
   m = wave_max(m);
   float s = 0.0f;
   if (head == 0) {
-    for (int i = lane; i < k; i += 64) s += expf(z[i] - m);
+#pragma unroll
+    for (int j = 0; j < KREG; ++j) {
+      if (lane + 64 * j < k) {
+        zr[j] = expf(zr[j] - m);
+        s += zr[j];
+      }
+    }
+    for (int i = lane + 64 * KREG; i < k; i += 64) s += expf(z[i] - m);
     s = wave_sum(s);
   }
   float best = -INFINITY;
   int bi = 0x7fffffff;
-  for (int i = lane; i < k; i += 64) {
-    const float p = head == 0 ? expf(z[i] - m) / s : 1.0f / (1.0f + expf(-z[i]));
+  auto take = [&](int i, float p) {
     if (probs) probs[clip * k + i] = p;
     if (p > best) {   // first occurrence within the lane's strided subset
       best = p;
       bi = i;
     }
+  };
+#pragma unroll
+  for (int j = 0; j < KREG; ++j) {
+    const int i = lane + 64 * j;
+    if (i < k) take(i, head == 0 ? zr[j] / s : 1.0f / (1.0f + expf(-zr[j])));
   }
+  for (int i = lane + 64 * KREG; i < k; i += 64)
+    take(i, head == 0 ? expf(z[i] - m) / s : 1.0f / (1.0f + expf(-z[i])));
   // wave argmax, ties -> lowest index (numpy argmax)
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
