@@ -136,6 +136,11 @@ struct mmla_ctx {
   bool sifin = true;
   // fused SI pipeline: si_fe writes 40-float feature rows for the stem (env MMLA_NO_SIPAD=1: 39)
   bool si_pad_feat = true;
+  // batches of <= lstm_split_max clips: the 3xFP16 BiLSTM with each direction's hidden units on eight workgroups
+  // (nets.hip bilstm_h3_split_kernel); env MMLA_NO_LSTM_SPLIT=1 at create: one workgroup per direction
+  bool lstm_split = true;
+  // measured (tools/lat_split_sweep.py): OD 1.62 -> 1.53 ms at 128 clips, even at 192, +1 % at 256
+  int lstm_split_max = 128;   // env MMLA_LSTM_SPLIT_MAX (A/B; the kernel takes up to 256)
   // 3xFP16 range guard: kernels set range_dev[0] (device-pointer calls; sticky until
   // mmla_range_check) or range_dev[1] (host-pointer micro-batches: re-run in exact f32) when an
   // operand they split into fp16 is >= 65504 in magnitude or not finite
@@ -313,7 +318,7 @@ enum Slot {
   S_PCM = 0, S_LENS, S_IMG, S_X, S_T1, S_T2, S_T3, S_SEQ, S_HOUT, S_LOGIT, S_FEAT, S_SILENT,
   S_OUT0, S_OUT1, S_OUT2, S_OUT3, S_IN, S_FESCR,
   S_NR_S, S_NR_BITS, S_NR_FMAX, S_NR_FRAMES, S_NR_ITEMS, S_NR_Y, S_NR_ROWS,
-  S_VAD_SPEECH, S_VAD_OUT, S_VAD_LENS, S_RS_TR, S_RS_WIN
+  S_VAD_SPEECH, S_VAD_OUT, S_VAD_LENS, S_RS_TR, S_RS_WIN, S_LSTM
 };
 
 // ---- weights -------------------------------------------------------------------------------------
@@ -725,6 +730,14 @@ double lstm_flops(int64_t n, int T, int D) { return 2.0 * n * T * 2 * (256.0 + D
 
 // BiLSTM on the 3xFP16 path when enabled (exact-f32 MFMA kernel otherwise)
 hipError_t lstm_run(mmla_ctx* c, const LstmW& L, const float* seq, int64_t n, int T, float* out) {
+  if (c->precision == MMLA_PREC_F16X3 && L.wth[0] && c->lstm_split &&
+      n <= std::min(c->lstm_split_max, bilstm_h3_split_max_clips())) {
+    void* ws = nullptr;   // small batches (the real-time calls): each direction over eight CUs
+    if (ws_get(c, S_LSTM, bilstm_h3_split_ws_bytes(), &ws) != MMLA_OK) return hipErrorOutOfMemory;
+    return bilstm_h3_split_launch(seq, (int)n, T, 128, L.wth[0], L.wtl[0], L.wth[1], L.wtl[1],
+                                  L.bias[0], L.bias[1], out, c->range_ptr, L.ws[0], L.ws[1], ws,
+                                  c->stream);
+  }
   if (c->precision == MMLA_PREC_F16X3 && L.wth[0])
     return bilstm_h3_launch(seq, (int)n, T, 128, L.wth[0], L.wtl[0], L.wth[1], L.wtl[1], L.bias[0],
                             L.bias[1], out, c->range_ptr, L.ws[0], L.ws[1], c->stream);
@@ -1089,6 +1102,8 @@ int mmla_create(int device, mmla_ctx** out) {
   if (const char* su = std::getenv("MMLA_NO_SIU")) c->siu = std::atoi(su) == 0;
   if (const char* sp = std::getenv("MMLA_NO_SIPU")) c->sipu = std::atoi(sp) == 0;
   if (const char* sf = std::getenv("MMLA_NO_SIFIN")) c->sifin = std::atoi(sf) == 0;
+  if (const char* ls = std::getenv("MMLA_NO_LSTM_SPLIT")) c->lstm_split = std::atoi(ls) == 0;
+  if (const char* lm = std::getenv("MMLA_LSTM_SPLIT_MAX")) c->lstm_split_max = std::atoi(lm);
   if (const char* sd = std::getenv("MMLA_NO_SIPAD")) c->si_pad_feat = std::atoi(sd) == 0;
   // a BLOCKING stream: it orders with the legacy default (NULL) stream, on which PyTorch's default
   // stream enqueues -- so a device-pointer call sees tensors a torch kernel or copy just produced

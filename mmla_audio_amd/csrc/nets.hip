@@ -462,6 +462,187 @@ __global__ void __launch_bounds__(512, (LSTM_W4 && MT == 1) ? 4 : 2) bilstm_h3_k
   if (rbad && range_flag) *range_flag = 1;
 }
 
+// ---- small-batch BiLSTM: a direction's hidden units over eight CUs ------------------------------
+// bilstm_h3_kernel<128,1> with n <= 32 runs each direction as ONE workgroup: every step streams the
+// direction's 1.5 MB of B fragments through one CU's L2 port (the batch-1 real-time call's largest
+// kernel).  Here the direction runs on eight workgroups, workgroup w owning bilstm_h3_kernel wave w's
+// 32 hidden units, and inside it wave g owns gate g: the wave's B fragments for one gate (24 k-steps
+// x hi / lo, 192 VGPRs) are loaded ONCE and stay in registers for all T steps, so a step streams no
+// weights at all.  Per step: the 72 MFMAs of the wave's gate (the same accumulator sequence as
+// bilstm_h3_kernel's gate-ahead loop), the four gates' pre-activations exchanged through LDS, the
+// gate math (each thread owns 4 of the 32 x 32 units and their c-state), and the 32 x 256 h_{t-1}
+// planes (fp16 hi / lo, 32 KB) exchanged through HBM: each workgroup publishes its 32 columns into
+// xbuf[dir][s & 1] and bumps sync[dir] (release fence at agent scope: the eight workgroups sit on
+// different XCDs, whose L2s are not coherent with each other), then waits for the counter to reach
+// 8 (s + 1) (acquire) before reading all 256 columns.  Outputs are bit-identical to
+// bilstm_h3_kernel (tests/test_gpu_batching.py).  Batches of up to 8 x 32 clips: one 32-row tile per
+// grid z, with its own counters sync[2 tile + dir] (zero at launch: bilstm_h3_split_launch clears them
+// on the stream) and exchange buffers.  Waits are bounded at LSTM_SPLIT_SPIN polls: a workgroup that
+// gives up sets sync[63], writes NaN for its units and exits, so the grid always drains.
+constexpr int LSTM_SPLIT_ROWS = 32;
+constexpr int LSTM_SPLIT_SPIN = 1 << 22;
+// up to 8 row tiles of 32 clips (grid z): at most 128 workgroups, so all of them are resident at once
+constexpr int LSTM_SPLIT_TILES = 8;
+
+template <int D>
+__global__ void __launch_bounds__(256, 1) bilstm_h3_split_kernel(const float* __restrict__ seq, int n, int T,
+                                                                 const uint16_t* __restrict__ wfh,
+                                                                 const uint16_t* __restrict__ wfl,
+                                                                 const uint16_t* __restrict__ wbh,
+                                                                 const uint16_t* __restrict__ wbl,
+                                                                 const float* __restrict__ bf,
+                                                                 const float* __restrict__ bb,
+                                                                 float* __restrict__ out,
+                                                                 int* __restrict__ range_flag,
+                                                                 float ws_f, float ws_b, int* sync,
+                                                                 _Float16* xbuf) {
+  constexpr int K = LSTM_U + D;
+  constexpr int KST = K / 16;
+  constexpr int LDA = K + 8;
+  constexpr int ROWS = LSTM_SPLIT_ROWS;
+  constexpr int PLANE = ROWS * LSTM_U;   // fp16 per h plane
+  constexpr int NTH = 256;
+  __shared__ __attribute__((aligned(16))) _Float16 Ahi[ROWS * LDA];
+  __shared__ __attribute__((aligned(16))) _Float16 Alo[ROWS * LDA];
+  __shared__ float G[4][16][64];   // the four gates' accumulators, [gate][register][lane]
+  const int tid = threadIdx.x, lane = tid & 63, gate = tid >> 6;
+  const int grp = blockIdx.x;   // hidden units [32 grp, 32 grp + 32) (bilstm_h3_kernel's wave grp)
+  const int dir = blockIdx.y;
+  const uint16_t* __restrict__ Wh = dir == 0 ? wfh : wbh;
+  const uint16_t* __restrict__ Wl = dir == 0 ? wfl : wbl;
+  const float* __restrict__ B = dir == 0 ? bf : bb;
+  const float WS = dir == 0 ? ws_f : ws_b;
+  const float LSTM_UNSCALE = 1.0f / (WS * LSTM_AS);
+  const int tile = blockIdx.z;   // clips [32 tile, 32 tile + 32)
+  const int nr = n - 32 * tile;   // rows of this tile that are clips
+  int* cnt = sync + 2 * tile + dir;
+  _Float16* xh = xbuf + (size_t)(2 * tile + dir) * 2 * 2 * PLANE;   // [parity][hi, lo][row][256]
+  seq += (int64_t)32 * tile * T * D;
+  out += (int64_t)32 * tile * 512;
+  const int col = 32 * grp + (lane & 31);
+  const int koff = 8 * (lane >> 5);
+  constexpr size_t GS = (size_t)LSTM_U * K;
+
+  // the wave's gate of the group's B fragments, resident for the launch
+  const uint32_t lob = (uint32_t)(grp * KST * 512 + lane * 8) * 2u;
+  const __amdgpu_buffer_rsrc_t rh = lstm_rsrc(Wh, (uint32_t)(4 * GS * 2));
+  const __amdgpu_buffer_rsrc_t rl = lstm_rsrc(Wl, (uint32_t)(4 * GS * 2));
+  f16x8 bh[KST], bl[KST];
+#pragma unroll
+  for (int ks = 0; ks < KST; ++ks) {
+    const int uo = (int)((gate * GS + 512 * (size_t)ks) * 2);
+    bh[ks] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(rh, lob, uo, 0));
+    bl[ks] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(rl, lob, uo, 0));
+  }
+  const float bias = B[gate * LSTM_U + col] * (WS * LSTM_AS);
+
+  for (int e = tid; e < ROWS * LSTM_U / 8; e += NTH) {   // h_{-1} = 0
+    const int r = e / (LSTM_U / 8), q = e - r * (LSTM_U / 8);
+    *reinterpret_cast<f16x8*>(Ahi + r * LDA + 8 * q) = f16x8{};
+    *reinterpret_cast<f16x8*>(Alo + r * LDA + 8 * q) = f16x8{};
+  }
+  bool rbad = false;
+  auto stage_x = [&](int t) {   // x_t -> A[:, 256:256+D], as bilstm_h3_kernel
+    for (int e = tid; e < ROWS * D / 4; e += NTH) {
+      const int r = e / (D / 4), d4 = e - r * (D / 4);
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (r < nr) v = *reinterpret_cast<const float4*>(seq + ((int64_t)r * T + t) * D + 4 * d4);
+      rbad |= !(fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))) <
+                65504.0f / LSTM_AS);
+      _Float16 h0, h1, h2, h3, l0, l1, l2, l3;
+      split1(v.x, h0, l0);
+      split1(v.y, h1, l1);
+      split1(v.z, h2, l2);
+      split1(v.w, h3, l3);
+      const f16x4 hv = {h0, h1, h2, h3}, lv = {l0, l1, l2, l3};
+      *reinterpret_cast<f16x4*>(Ahi + r * LDA + LSTM_U + 4 * d4) = hv;
+      *reinterpret_cast<f16x4*>(Alo + r * LDA + LSTM_U + 4 * d4) = lv;
+    }
+  };
+  const _Float16* arow_h = Ahi + (lane & 31) * LDA + koff;
+  const _Float16* arow_l = Alo + (lane & 31) * LDA + koff;
+  float cst[4] = {0.0f, 0.0f, 0.0f, 0.0f};   // units (register 4 gate + j, lane)
+
+  stage_x(dir == 0 ? 0 : T - 1);
+  bool dead = false;
+  for (int s = 0; s < T; ++s) {
+    if (s > 0) {   // every workgroup's h_{t-1} published
+      int it = 0;
+      while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < 8 * s) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++it == LSTM_SPLIT_SPIN) break;
+      }
+      if (it == LSTM_SPLIT_SPIN) {
+        dead = true;
+        break;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      const _Float16* src = xh + (size_t)((s - 1) & 1) * 2 * PLANE;
+      for (int e = tid; e < 2 * PLANE / 8; e += NTH) {   // planes hi, lo: 16-B chunks, row-major
+        const int hl = e / (PLANE / 8), rem = e - hl * (PLANE / 8);
+        const int r = rem / (LSTM_U / 8), q = rem - r * (LSTM_U / 8);
+        const f16x8 v = *reinterpret_cast<const f16x8*>(src + (size_t)e * 8);
+        *reinterpret_cast<f16x8*>((hl ? Alo : Ahi) + r * LDA + 8 * q) = v;
+      }
+    }
+    __syncthreads();
+    f32x16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = bias;
+#pragma unroll
+    for (int ks = 0; ks < KST; ++ks) {
+      const f16x8 ah = *reinterpret_cast<const f16x8*>(arow_h + 16 * ks);
+      const f16x8 al = *reinterpret_cast<const f16x8*>(arow_l + 16 * ks);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[ks], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl[ks], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[ks], acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) G[gate][r][lane] = acc[r];
+    __syncthreads();   // the gates are in LDS; every wave has read h_{t-1} and x_t
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int r = 4 * gate + j;
+      const int row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      const float ig = sigm_f(G[0][r][lane] * LSTM_UNSCALE);
+      const float fg = sigm_f(G[1][r][lane] * LSTM_UNSCALE);
+      const float gg = tanh_f(G[2][r][lane] * LSTM_UNSCALE);
+      const float og = sigm_f(G[3][r][lane] * LSTM_UNSCALE);
+      const float c = fg * cst[j] + ig * gg;
+      cst[j] = c;
+      const float h = og * tanh_f(c);
+      if (s == T - 1 && row < nr) out[(int64_t)row * 512 + dir * LSTM_U + col] = h;
+      _Float16 hh, hl;
+      split1(h, hh, hl);
+      Ahi[row * LDA + col] = hh;
+      Alo[row * LDA + col] = hl;
+    }
+    if (s + 1 < T) {
+      __syncthreads();
+      {   // this group's 32 columns of both planes -> xbuf[dir][s & 1]: one 16-B chunk per thread
+        _Float16* dst = xh + (size_t)(s & 1) * 2 * PLANE;
+        const int hl = tid / (ROWS * 4), rem = tid - hl * (ROWS * 4);
+        const int r = rem >> 2, q = rem & 3;
+        const f16x8 v = *reinterpret_cast<const f16x8*>((hl ? Alo : Ahi) + r * LDA + 32 * grp + 8 * q);
+        *reinterpret_cast<f16x8*>(dst + (size_t)hl * PLANE + r * LSTM_U + 32 * grp + 8 * q) = v;
+      }
+      static_assert(2 * ROWS * 4 == NTH, "one publish chunk per thread");
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");   // each wave: its stores, then L2 written back
+      __syncthreads();
+      if (tid == 0) __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      stage_x(dir == 0 ? s + 1 : T - 2 - s);   // under the other workgroups' arrival
+    }
+  }
+  if (dead) {
+    if (tid == 0) __hip_atomic_store(sync + 63, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int j = 0; j < 4; ++j) {
+      const int r = 4 * gate + j, row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      if (row < nr) out[(int64_t)row * 512 + dir * LSTM_U + col] = __builtin_nanf("");
+    }
+  }
+  if (rbad && range_flag) *range_flag = 1;
+}
+
 __global__ void od_head_kernel(const float* __restrict__ h, int n, const float* __restrict__ w,
                                const float* __restrict__ b, float* __restrict__ probs,
                                int32_t* __restrict__ argmax, const int32_t* __restrict__ lens,
@@ -628,6 +809,27 @@ hipError_t bilstm_h3_launch(const float* seq, int n, int T, int D, const uint16_
   }
   hipLaunchKernelGGL((bilstm_h3_kernel<128, 1>), dim3(blocks_for(n, LSTM_ROWS), 2), dim3(512), 0, s,
                      seq, n, T, wfh, wfl, wbh, wbl, bf, bb, out, range_flag, ws_fwd, ws_bwd);
+  return hipGetLastError();
+}
+
+size_t bilstm_h3_split_ws_bytes() {
+  return 256 + (size_t)LSTM_SPLIT_TILES * 2 * 2 * 2 * LSTM_SPLIT_ROWS * LSTM_U * 2;
+}
+int bilstm_h3_split_max_clips() { return LSTM_SPLIT_TILES * LSTM_SPLIT_ROWS; }
+
+hipError_t bilstm_h3_split_launch(const float* seq, int n, int T, int D, const uint16_t* wfh,
+                                  const uint16_t* wfl, const uint16_t* wbh, const uint16_t* wbl,
+                                  const float* bf, const float* bb, float* out, int* range_flag,
+                                  float ws_fwd, float ws_bwd, void* ws, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  if (D != 128 || n > LSTM_SPLIT_TILES * LSTM_SPLIT_ROWS || T < 1) return hipErrorInvalidValue;
+  const int tiles = (n + LSTM_SPLIT_ROWS - 1) / LSTM_SPLIT_ROWS;
+  int* sync = static_cast<int*>(ws);
+  _Float16* xbuf = reinterpret_cast<_Float16*>(static_cast<char*>(ws) + 256);
+  const hipError_t e = hipMemsetAsync(sync, 0, 64 * sizeof(int), s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL((bilstm_h3_split_kernel<128>), dim3(8, 2, tiles), dim3(256), 0, s, seq, n, T, wfh, wfl,
+                     wbh, wbl, bf, bb, out, range_flag, ws_fwd, ws_bwd, sync, xbuf);
   return hipGetLastError();
 }
 

@@ -119,3 +119,31 @@ def test_large_batches_match_batch_one(ctx):
     for i in (1, 4100, 8198):
         p1, a1, _ = ctx.si_pipeline(pcm[i:i + 1])
         assert np.array_equal(p1[0], p_all[i]) and a1[0] == a_all[i]
+
+
+@pytest.mark.parametrize('n', [1, 5, 32, 33, 200, 256])
+def test_small_batch_lstm_split_bit_identical(monkeypatch, n):
+    """Batches of <= 256 clips run the BiLSTM with each direction's hidden units spread over eight
+    workgroups per 32 clips (nets.hip bilstm_h3_split_kernel, h exchanged through HBM each step); env
+    MMLA_NO_LSTM_SPLIT=1 keeps one workgroup per direction.  Same bits, OD and SI, no NaN (a
+    workgroup that gave up waiting writes NaN)."""
+    from mmla_audio_amd import _lib, weights
+    W = weights.synthetic(weights.OD, seed=23)
+    Ws = weights.synthetic(weights.SI, seed=24, n_classes=630)
+    od = synth.batch(1900 + n, n, 40000)
+    si = [synth.clip(2000 + i, 24000 if i % 3 else 17000) for i in range(n)]
+    out = []
+    for flag in ('0', '1'):
+        monkeypatch.setenv('MMLA_NO_LSTM_SPLIT', flag)
+        monkeypatch.setenv('MMLA_LSTM_SPLIT_MAX', '256')   # the kernel's limit, past the default
+        c = _lib.Context(0)
+        monkeypatch.delenv('MMLA_NO_LSTM_SPLIT')
+        monkeypatch.delenv('MMLA_LSTM_SPLIT_MAX')
+        c.load_weights(weights.OD, weights.pack(weights.OD, W), 2)
+        c.load_weights(weights.SI, weights.pack(weights.SI, Ws, 630), 630, _lib.HEAD_SOFTMAX)
+        out.append((c.od_pipeline(od), c.si_pipeline(si)))
+    (po, ao, _), (ps, as_, _) = out[0]
+    (qo, bo, _), (qs, bs, _) = out[1]
+    assert np.isfinite(po).all() and np.isfinite(ps).all()
+    assert np.array_equal(po, qo) and np.array_equal(ao, bo)
+    assert np.array_equal(ps, qs) and np.array_equal(as_, bs)

@@ -15,7 +15,10 @@ ctx.load_weights(weights.SI, weights.pack(weights.SI, weights.synthetic(weights.
                  _lib.HEAD_SIGMOID)
 for name, fn, pcm in (('od_pipeline', ctx.od_pipeline, synth.batch(3, 1, 40960)),
                       ('si_pipeline', ctx.si_pipeline, synth.batch(4, 1, 40960)),
-                      ('od_pipeline x8', ctx.od_pipeline, synth.batch(5, 8, 40960))):
+                      ('od_pipeline x8', ctx.od_pipeline, synth.batch(5, 8, 40960)),
+                      ('od_pipeline x64', ctx.od_pipeline, synth.batch(6, 64, 40960)),
+                      ('od_pipeline x256', ctx.od_pipeline, synth.batch(7, 256, 40960)),
+                      ('si_pipeline x256', ctx.si_pipeline, synth.batch(8, 256, 40960))):
     for _ in range(5):
         fn(pcm)
     ts = []
