@@ -147,3 +147,30 @@ def test_small_batch_lstm_split_bit_identical(monkeypatch, n):
     assert np.isfinite(po).all() and np.isfinite(ps).all()
     assert np.array_equal(po, qo) and np.array_equal(ao, bo)
     assert np.array_equal(ps, qs) and np.array_equal(as_, bs)
+
+
+@pytest.mark.parametrize('n', [1, 3, 40])
+def test_host_mapped_outputs_bit_identical(monkeypatch, n):
+    """Small host-pointer calls write their outputs and the range flag into host-mapped memory
+    (capi.cpp pin_small); env MMLA_NO_PIN_OUT=1 stages them in HBM and copies them back.  Same
+    results for the pipelines, the front-end images and the network-only entry."""
+    from mmla_audio_amd import _lib, weights
+    W = weights.synthetic(weights.OD, seed=25)
+    Ws = weights.synthetic(weights.SI, seed=26, n_classes=8)
+    od = synth.batch(2100 + n, n, 40000)
+    si = [synth.clip(2200 + i, 24000 if i % 2 else 3000) for i in range(n)]
+    res = []
+    for flag in ('0', '1'):
+        monkeypatch.setenv('MMLA_NO_PIN_OUT', flag)
+        c = _lib.Context(0)
+        monkeypatch.delenv('MMLA_NO_PIN_OUT')
+        c.load_weights(weights.OD, weights.pack(weights.OD, W), 2)
+        c.load_weights(weights.SI, weights.pack(weights.SI, Ws, 8), 8, _lib.HEAD_SIGMOID)
+        f = c.od_features(od)
+        res.append((c.od_pipeline(od), c.si_pipeline(si), f, c.od_forward(f['img'])))
+    (a_od, a_si, a_f, a_x), (b_od, b_si, b_f, b_x) = res
+    for u, v in zip(a_od + a_si, b_od + b_si):
+        assert np.array_equal(u, v)
+    for k in a_f:   # a silent clip's normalize_matrix is 0/0 = NaN (the reference's too)
+        assert np.array_equal(a_f[k], b_f[k], equal_nan=a_f[k].dtype.kind == 'f'), k
+    assert np.array_equal(a_x, b_x)
