@@ -156,6 +156,7 @@ struct mmla_ctx {
   int* range_map_dev = nullptr;   // device view of the same word
   char* pin_out = nullptr;        // kPinSlots x kPinSlotBytes, host view
   char* pin_out_dev = nullptr;
+  char* pin_in = nullptr;         // kPinInBytes of pinned input staging: one DMA for PCM + lens
   int* range_ptr = nullptr;                 // what the current launches write (null: unguarded)
   int64_t range_reruns = 0;
   bool od_f32_only = false, si_f32_only = false;   // weights outside the fp16 range
@@ -479,6 +480,10 @@ void free_allocs(std::vector<void*>& al) {
 
 // ---- PCM staging -------------------------------------------------------------------------------
 
+// host-pinned staging of small host-pointer calls (mmla_ctx::pin_small)
+constexpr size_t kPinSlotBytes = 64u << 10;
+constexpr size_t kPinInBytes = 1u << 20;
+
 template <typename T>
 struct PcmT {
   const T* p;
@@ -500,6 +505,26 @@ int stage_pcm(mmla_ctx* c, const T* pcm, int64_t c0, int64_t cnt, int64_t stride
   int64_t width = lens ? std::min<int64_t>(need, stride) : std::min<int64_t>(need, clip_len);
   if (width < 1) width = 1;
   void* dp = nullptr;
+  const bool overlap = !lens && stride < width;
+  const size_t pbytes = (size_t)(overlap ? (cnt - 1) * stride + width : cnt * width) * sizeof(T);
+  const size_t loff = (pbytes + 255) & ~(size_t)255;
+  if (c->pin_small && c->pin_in && loff + (lens ? cnt * sizeof(int32_t) : 0) <= kPinInBytes) {
+    // small calls: gather into pinned memory on the host, one asynchronous DMA (host-mode bodies
+    // end with a stream synchronisation, so the staging is free again when the next one starts)
+    if (overlap) {
+      std::memcpy(c->pin_in, pcm + c0 * stride, pbytes);
+    } else {
+      for (int64_t i = 0; i < cnt; ++i)
+        std::memcpy(c->pin_in + (size_t)i * width * sizeof(T), pcm + (c0 + i) * stride, width * sizeof(T));
+    }
+    const size_t tot = loff + (lens ? cnt * sizeof(int32_t) : 0);
+    if (lens) std::memcpy(c->pin_in + loff, lens + c0, cnt * sizeof(int32_t));
+    CHK(ws_get(c, S_PCM, tot, &dp));
+    HIPCHK(c, hipMemcpyAsync(dp, c->pin_in, tot, hipMemcpyHostToDevice, c->stream));
+    const int32_t* dl = lens ? reinterpret_cast<const int32_t*>(static_cast<char*>(dp) + loff) : nullptr;
+    *out = {static_cast<T*>(dp), overlap ? stride : width, dl, (int32_t)std::min<int64_t>(clip_len, width)};
+    return MMLA_OK;
+  }
   if (!lens && stride < width) {
     // overlapping windows of one signal (segmentation with step < window): copy the covered span
     // once and let the kernels read window c at c * stride
@@ -526,7 +551,6 @@ int stage_pcm(mmla_ctx* c, const T* pcm, int64_t c0, int64_t cnt, int64_t stride
 
 // device destination for an output chunk: the caller's pointer (device mode), a host-mapped slot
 // (small host-mode outputs, mmla_ctx::pin_small) or a staging slot in HBM
-constexpr size_t kPinSlotBytes = 64u << 10;
 constexpr int kPinSlots = 4;   // S_OUT0 .. S_OUT3
 template <typename T>
 int out_ptr(mmla_ctx* c, T* user, int64_t off, size_t count, bool dev, int slot, T** d) {
@@ -1160,7 +1184,8 @@ int mmla_create(int device, mmla_ctx** out) {
     if (hipHostMalloc(reinterpret_cast<void**>(&c->range_map), 64, fl) != hipSuccess ||
         hipHostGetDevicePointer(reinterpret_cast<void**>(&c->range_map_dev), c->range_map, 0) != hipSuccess ||
         hipHostMalloc(reinterpret_cast<void**>(&c->pin_out), kPinSlots * kPinSlotBytes, fl) != hipSuccess ||
-        hipHostGetDevicePointer(reinterpret_cast<void**>(&c->pin_out_dev), c->pin_out, 0) != hipSuccess) {
+        hipHostGetDevicePointer(reinterpret_cast<void**>(&c->pin_out_dev), c->pin_out, 0) != hipSuccess ||
+        hipHostMalloc(reinterpret_cast<void**>(&c->pin_in), kPinInBytes, hipHostMallocDefault) != hipSuccess) {
       mmla_destroy(c);
       return MMLA_E_HIP;
     }
@@ -1206,6 +1231,7 @@ int mmla_destroy(mmla_ctx* c) {
   if (c->range_host) (void)hipHostFree(c->range_host);
   if (c->range_map) (void)hipHostFree(c->range_map);
   if (c->pin_out) (void)hipHostFree(c->pin_out);
+  if (c->pin_in) (void)hipHostFree(c->pin_in);
   (void)prof_collect(c);
   for (hipEvent_t e : c->prof_pool) (void)hipEventDestroy(e);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);

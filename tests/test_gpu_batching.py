@@ -151,9 +151,11 @@ def test_small_batch_lstm_split_bit_identical(monkeypatch, n):
 
 @pytest.mark.parametrize('n', [1, 3, 40])
 def test_host_mapped_outputs_bit_identical(monkeypatch, n):
-    """Small host-pointer calls write their outputs and the range flag into host-mapped memory
-    (capi.cpp pin_small); env MMLA_NO_PIN_OUT=1 stages them in HBM and copies them back.  Same
-    results for the pipelines, the front-end images and the network-only entry."""
+    """Small host-pointer calls gather their PCM (+ lens) into pinned memory for one DMA and write
+    their outputs and the range flag into host-mapped memory (capi.cpp pin_small); env
+    MMLA_NO_PIN_OUT=1 copies from pageable memory and stages outputs in HBM.  Same results for the
+    pipelines, ragged (lens) input, overlapping windows, the front-end images and the network-only
+    entry."""
     from mmla_audio_amd import _lib, weights
     W = weights.synthetic(weights.OD, seed=25)
     Ws = weights.synthetic(weights.SI, seed=26, n_classes=8)
@@ -167,8 +169,12 @@ def test_host_mapped_outputs_bit_identical(monkeypatch, n):
         c.load_weights(weights.OD, weights.pack(weights.OD, W), 2)
         c.load_weights(weights.SI, weights.pack(weights.SI, Ws, 8), 8, _lib.HEAD_SIGMOID)
         f = c.od_features(od)
-        res.append((c.od_pipeline(od), c.si_pipeline(si), f, c.od_forward(f['img'])))
-    (a_od, a_si, a_f, a_x), (b_od, b_si, b_f, b_x) = res
+        # overlapping windows of one signal (segmentation with step < window): the span path
+        g = c.od_features_strided(synth.clip(2300, 80000), n, 1000, 40000, db=False, norm=False)
+        res.append((c.od_pipeline(od), c.si_pipeline(si), f, c.od_forward(f['img']), g))
+    (a_od, a_si, a_f, a_x, a_g), (b_od, b_si, b_f, b_x, b_g) = res
+    for k in a_g:
+        assert np.array_equal(a_g[k], b_g[k]), k
     for u, v in zip(a_od + a_si, b_od + b_si):
         assert np.array_equal(u, v)
     for k in a_f:   # a silent clip's normalize_matrix is 0/0 = NaN (the reference's too)
