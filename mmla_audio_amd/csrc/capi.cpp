@@ -1760,7 +1760,12 @@ int mmla_si_pipeline(mmla_ctx* c, const int16_t* pcm, int64_t n, int64_t stride,
       const int ldf = c->precision == MMLA_PREC_F16X3 && c->si.stem.wh && c->si.stem.cin_pad > SI_D &&
                               c->si_pad_feat ? SI_D + 1 : SI_D;
       CHK(ws_get(c, S_FEAT, cnt * SI_T * ldf * sizeof(float), &pf));
-      CHK(ws_get(c, S_SILENT, cnt, &ps));
+      uint8_t* pso = nullptr;   // host mode: the caller's 'silent' flags through an output slot
+      if (!dev && silent) CHK(out_ptr(c, silent, c0, cnt, dev, S_OUT2, &pso));
+      if (pso)
+        ps = pso;
+      else
+        CHK(ws_get(c, S_SILENT, cnt, &ps));
       SiFeArgs a{};
       a.pcm = p.p;
       a.clip_stride = p.stride;
@@ -1782,7 +1787,7 @@ int mmla_si_pipeline(mmla_ctx* c, const int16_t* pcm, int64_t n, int64_t stride,
         if (dev)
           HIPCHK(c, hipMemcpyAsync(silent + c0, a.silent, cnt, hipMemcpyDeviceToDevice, c->stream));
         else
-          HIPCHK(c, hipMemcpyAsync(silent + c0, a.silent, cnt, hipMemcpyDeviceToHost, c->stream));
+          CHK(copy_back(c, silent, c0, pso, cnt, dev));
       }
       if (!dev) HIPCHK(c, hipStreamSynchronize(c->stream));
       return MMLA_OK;
