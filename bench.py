@@ -205,9 +205,13 @@ def parity_sample(ctx, wl, pcm, probs, argmax, W, mb, clip_len, k=24, fe_out=Non
         zc = fe_out[1][idx].cpu().numpy()
     elif wl == 'od_pipeline':
         nrm = torch.empty((len(idx), 128, 151), dtype=torch.float32, device='cuda')
+        gim = torch.empty((len(idx), 128, 151, 3), dtype=torch.uint8, device='cuda')
         ctx.od_features_dev(sub.data_ptr(), len(idx), clip_len, clip_len, norm=nrm.data_ptr())
+        # the image the pipeline's network reads (the fused pipeline = od_forward_u8 on it, bit for bit)
+        ctx.od_features_dev(sub.data_ptr(), len(idx), clip_len, clip_len, img=gim.data_ptr())
         torch.cuda.synchronize()
         norm = nrm.cpu().numpy()
+        gimg = gim.cpu().numpy()
         zc = None
     if wl in ('od_pipeline', 'od_features'):
         feats = [od_fe.od_features(host[j]) for j in range(len(idx))]
@@ -224,7 +228,17 @@ def parity_sample(ctx, wl, pcm, probs, argmax, W, mb, clip_len, k=24, fe_out=Non
         if zc is not None:
             out['zcr_count_mismatch_clips'] = zbad
         if wl == 'od_pipeline':
-            ref = Nets(W).od_forward(np.stack([f['png_rgb'] for f in feats]).astype(np.float32))
+            oimg = np.stack([f['png_rgb'] for f in feats])
+            net = Nets(W)
+            ref = net.od_forward(oimg.astype(np.float32))
+            # the network alone: the oracle net on the GPU's OWN image (the
+            # end-to-end figure also carries the image's permitted 1-LSB pixel values, which the
+            # seeded net amplifies)
+            ref_net = net.od_forward(gimg.astype(np.float32))
+            lsb = np.abs(gimg.astype(np.int16) - oimg.astype(np.int16))
+            out['img_lsb_pixels'] = int((lsb > 0).sum())
+            out['img_pixel_values'] = int(lsb.size)
+            out['img_max_lsb'] = int(lsb.max())
     else:
         feat = torch.empty((len(idx), 256, 39), dtype=torch.float32, device='cuda')
         ctx.si_features_dev(sub.data_ptr(), len(idx), clip_len, clip_len, feat.data_ptr())
@@ -237,6 +251,19 @@ def parity_sample(ctx, wl, pcm, probs, argmax, W, mb, clip_len, k=24, fe_out=Non
         gp = probs[idx].cpu().numpy()
         ga = argmax[idx].cpu().numpy()
         agree, disagree, ties = compare.argmax_report(gp, ref)
+        if wl == 'od_pipeline':
+            with np.errstate(divide='ignore'):
+                e2e = np.abs(np.log(gp.astype(np.float64)) - np.log(ref)).max(1)
+                own = np.abs(np.log(gp.astype(np.float64)) - np.log(ref_net)).max(1)
+            j = int(e2e.argmax())
+            out.update({'logp_err_net': compare.logp_err(gp, ref_net),
+                        'logp_err_net_bar': compare.LOGP_TOL,
+                        'worst_clip': {'index': int(idx[j]), 'logp_err_e2e': float(e2e[j]),
+                                       'logp_err_net': float(own[j]),
+                                       'img_lsb_pixels': int((lsb[j] > 0).sum())},
+                        'logp_err_note': 'logp_max_abs_err = GPU pipeline vs the oracle net on the '
+                                         'ORACLE image (includes 1-LSB image differences); '
+                                         'logp_err_net = vs the oracle net on the GPU image'})
         out.update({'logp_max_abs_err': compare.logp_err(gp, ref), 'prob_max_abs_err': float(np.abs(gp - ref).max()),
                     'argmax_agree': agree, 'argmax_disagree_non_tie': disagree,
                     'argmax_matches_probs': bool(np.array_equal(ga, gp.argmax(1))),

@@ -58,6 +58,12 @@ typedef struct mmla_ctx mmla_ctx;
 
 int mmla_abi_version(void);
 
+/* CRC-32C (Castagnoli) of n bytes -> *crc (host only, no context or device): the checksum TF's
+ * tensor bundle stores per tensor (BundleEntryProto.crc32c, masked as LevelDB does; tfbundle.py
+ * verifies every tensor it loads from variables.data-*, replacing the check of
+ * tf.keras.models.load_model at record_on_pc.py:88 / SI record_on_pc.py:77). */
+int mmla_crc32c(const void* data, int64_t n, uint32_t* crc);
+
 /* Create a context on HIP device `device` (owns a stream, device workspaces and loaded weights). */
 int mmla_create(int device, mmla_ctx** out);
 int mmla_destroy(mmla_ctx* ctx);
@@ -69,7 +75,9 @@ const char* mmla_last_error(const mmla_ctx* ctx);
  * the work already enqueued on the old one, which still uses this context's workspaces. */
 int mmla_set_stream(mmla_ctx* ctx, void* hip_stream);
 /* Wait for the context stream; returns MMLA_E_RANGE (see mmla_range_check) if a device-pointer call
- * since the last check overflowed the fp16 range. */
+ * since the last check overflowed the fp16 range, MMLA_E_HIP if one ran the split BiLSTM (batches of
+ * <= 128 clips) and a workgroup of it timed out (NaN probabilities; host-pointer calls re-run such a
+ * micro-batch on the unsplit kernel instead, bit-identical). */
 int mmla_synchronize(mmla_ctx* ctx);
 /*
  * Arithmetic of the spatial convolutions (98 % of OD-NET FLOPs) and the BiLSTM:
@@ -85,7 +93,9 @@ int mmla_synchronize(mmla_ctx* ctx);
  *                   (counted by mmla_range_check); device-pointer calls report MMLA_E_RANGE from
  *                   the next mmla_range_check / mmla_synchronize.
  *   MMLA_PREC_F32   exact f32 MFMA (v_mfma_f32_32x32x2_f32), 1/5.3 of the throughput.
- * 1x1 shortcuts, dense heads and the front-ends are f32/f64 in both modes.
+ * The front-ends (OD f32, SI f64), the OD stem Conv2D(1x1), the OD Dense(2) head and the softmax /
+ * sigmoid are the same in both modes; under MMLA_PREC_F16X3 the strided 1x1 shortcuts (OD blocks 1,
+ * 4, 7; SI pool units) and the SI Dense(K) run 3xFP16 with the convolutions they are fused into.
  */
 enum mmla_precision { MMLA_PREC_F32 = 0, MMLA_PREC_F16X3 = 1 };
 int mmla_set_precision(mmla_ctx* ctx, int mode);
@@ -275,6 +285,12 @@ int mmla_debug_od_trace(mmla_ctx* ctx, const float* x, int64_t n, int stage, flo
 /* Debug (tests, tools): device address and size of internal workspace slot `slot` (0 and 0 when the
  * slot was never allocated), e.g. to check that no kernel of another call writes into it. */
 int mmla_debug_ws_slot(mmla_ctx* ctx, int slot, void** ptr, size_t* bytes);
+/* Debug (tests): recovery counters of the context so far (each nullable): host-pointer micro-batches
+ * re-run in exact f32 by the range guard, and host-pointer micro-batches re-run on the
+ * one-workgroup-per-direction BiLSTM because a workgroup of the split BiLSTM (batches <= 128 clips)
+ * timed out waiting for the others.  Env MMLA_DEBUG_LSTM_SPIN=<polls> at mmla_create bounds that
+ * wait (tests force the timeout path with 1). */
+int mmla_debug_counters(mmla_ctx* ctx, int64_t* f32_reruns, int64_t* lstm_split_reruns);
 /* ms[MMLA_NSTAGES], launches[MMLA_NSTAGES], work[MMLA_NSTAGES] (each nullable); reset != 0 clears */
 int mmla_profile_read(mmla_ctx* ctx, double* ms, int64_t* launches, double* work, int reset);
 

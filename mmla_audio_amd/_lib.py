@@ -36,6 +36,7 @@ SIGNATURES = {
     'mmla_nr_set_noise': [_P, _P, _I64, ctypes.c_int32, ctypes.c_uint32],
     'mmla_nr_reduce': [_P, _P, _I64, _I64, _I64, _P, ctypes.c_uint32],
     'mmla_abi_version': [],
+    'mmla_crc32c': [_P, _I64, ctypes.POINTER(_U32)],
     'mmla_create': [ctypes.c_int, ctypes.POINTER(_P)],
     'mmla_destroy': [_P],
     'mmla_set_stream': [_P, _P],
@@ -59,6 +60,7 @@ SIGNATURES = {
     'mmla_profile_read': [_P, _P, _P, _P, ctypes.c_int],
     'mmla_debug_od_trace': [_P, _P, _I64, ctypes.c_int, _P, _I64],
     'mmla_debug_ws_slot': [_P, ctypes.c_int, _P, _P],
+    'mmla_debug_counters': [_P, ctypes.POINTER(_I64), ctypes.POINTER(_I64)],
     'mmla_vad_reset': [_P, _I64, _I32],
     'mmla_vad_remove_silence': [_P, _P, _I64, _I64, _P, _I32, _I64, _P, _P, _P, _I32, _U32],
     'mmla_vad_collect': [_P, _P, _I64, _I64, _P, _I32, _P, _I32, _P, _P, _U32],
@@ -100,6 +102,17 @@ def load_library(path=LIB_PATH):
         lib.mmla_last_error.restype = ctypes.c_char_p
         _lib = lib
         return lib
+
+
+def crc32c(data):
+    """CRC-32C of a bytes-like object (mmla_crc32c; host only, no device needed)."""
+    lib = load_library()
+    buf = np.frombuffer(memoryview(data).cast('B'), np.uint8)
+    out = _U32()
+    rc = lib.mmla_crc32c(buf.ctypes.data if buf.size else None, buf.size, ctypes.byref(out))
+    if rc != MMLA_OK:
+        raise MmlaError(f'mmla_crc32c: {_ERRORS.get(rc, rc)}', rc)
+    return out.value
 
 
 def _ptr(a):
@@ -182,6 +195,14 @@ class Context:
         self._check(self.lib.mmla_range_check(self.h, ctypes.byref(n)), 'mmla_range_check')
         return n.value
 
+    def debug_counters(self):
+        """-> (host micro-batches re-run in exact f32, host micro-batches re-run on the unsplit
+        BiLSTM after a split-BiLSTM timeout) so far"""
+        a, b = _I64(), _I64()
+        self._check(self.lib.mmla_debug_counters(self.h, ctypes.byref(a), ctypes.byref(b)),
+                    'mmla_debug_counters')
+        return a.value, b.value
+
     def profile_enable(self, on=True):
         self._check(self.lib.mmla_profile_enable(self.h, int(bool(on))), 'mmla_profile_enable')
 
@@ -243,6 +264,8 @@ class Context:
         """n_streams fresh webrtcvad.Vad(mode) detectors (state kept in the context)."""
         self._check(self.lib.mmla_vad_reset(self.h, int(n_streams), int(mode)), 'mmla_vad_reset')
         self.vad_streams = int(n_streams)
+        # whoever tagged the detector before (post-processing _vad_owner) no longer owns it
+        self.vad_owner = None
 
     def vad_remove_silence(self, pcm, lens=None, items_per_stream=1):
         """save_wave_file(silence_remove=True) of every item: int16 [n, L] (or a list) ->

@@ -151,11 +151,15 @@ class AudioSegment:
 
     @property
     def rms(self):
-        """audioop.rms(data, 2): (unsigned int) sqrt(sum(x^2) / n) with a float64 running sum"""
+        """audioop.rms(data, 2): (unsigned int) sqrt(sum(x^2) / n) with a float64 running sum,
+        accumulated sample by sample in order as CPython's loop does (np.add.accumulate is that
+        sequential loop; np.sum's pairwise sum and an exact int64 sum differ from it once the sum
+        passes 2^53, i.e. after ~8.4 M full-scale samples)"""
         if self.data.size == 0:
             return 0
-        x = self.data.astype(np.int64)
-        return int(np.sqrt(float(np.sum(x * x)) / self.data.size))
+        x = self.data.astype(np.float64)
+        total = float(np.add.accumulate(x * x)[-1])
+        return int(np.sqrt(total / self.data.size))
 
     max_possible_amplitude = 2 ** 15
 

@@ -141,23 +141,29 @@ struct mmla_ctx {
   bool lstm_split = true;
   // measured (tools/lat_split_sweep.py): OD 1.62 -> 1.53 ms at 128 clips, even at 192, +1 % at 256
   int lstm_split_max = 128;   // env MMLA_LSTM_SPLIT_MAX (A/B; the kernel takes up to 256)
+  // test hook (env MMLA_DEBUG_LSTM_SPIN at create): the split BiLSTM's wait bound in polls (0 = default)
+  int lstm_spin = 0;
   // 3xFP16 range guard: kernels set range_dev[0] (device-pointer calls; sticky until
   // mmla_range_check) or range_dev[1] (host-pointer micro-batches: re-run in exact f32) when an
-  // operand they split into fp16 is >= 65504 in magnitude or not finite
+  // operand they split into fp16 is >= 65504 in magnitude or not finite.  The split BiLSTM's wait
+  // timeout (bilstm_h3_split_kernel) likewise: range_dev[3] (device-pointer calls, sticky) or
+  // range_dev[2] (host-pointer micro-batches: re-run on the one-workgroup-per-direction kernel)
   int* range_dev = nullptr;
-  int* range_host = nullptr;                // pinned copy of range_dev[1]
+  int* range_host = nullptr;                // pinned copy of range_dev[1..2]
   // small host-pointer calls (the real-time loops' batch-1 case): the range flag and the outputs live
   // in host-mapped coherent memory that the kernels write over the bus, so a micro-batch ends with one
   // stream synchronisation and host memcpys instead of three or four device-to-host copies, a flag
   // memset and a second synchronisation (each copy ≈ 20 µs of a 0.55 ms call).  env MMLA_NO_PIN_OUT=1
   // at create: staging slots in HBM + hipMemcpyAsync (A/B)
   bool pin_small = true;
-  int* range_map = nullptr;       // host view
-  int* range_map_dev = nullptr;   // device view of the same word
+  int* range_map = nullptr;       // host view: [0] range flag, [1] split-BiLSTM timeout
+  int* range_map_dev = nullptr;   // device view of the same words
   char* pin_out = nullptr;        // kPinSlots x kPinSlotBytes, host view
   char* pin_out_dev = nullptr;
   char* pin_in = nullptr;         // kPinInBytes of pinned input staging: one DMA for PCM + lens
   int* range_ptr = nullptr;                 // what the current launches write (null: unguarded)
+  int* timeout_ptr = nullptr;               // where the split BiLSTM reports a timeout (null: nowhere)
+  int64_t lstm_split_reruns = 0;
   int64_t range_reruns = 0;
   bool od_f32_only = false, si_f32_only = false;   // weights outside the fp16 range
   bool loading_f16_bad = false;                     // mmla_load_weights scratch
@@ -374,7 +380,9 @@ static float pick_wscale(const float* w, size_t n, bool* finite) {
     else m = std::max(m, a);
   }
   if (m == 0.0f || (m < 255.9f && m >= 0.0625f)) return 256.0f;
-  const int e = std::max(-100, std::min(100, (int)std::floor(std::log2(16384.0 / m))));
+  // e >= -126: the largest finite max |w| (< 2^128) needs e = -114, so after the clamp
+  // m * 2^e < 2^14 for every finite tensor and its fp16 hi half never overflows
+  const int e = std::max(-126, std::min(100, (int)std::floor(std::log2(16384.0 / m))));
   return std::ldexp(1.0f, e);
 }
 
@@ -643,14 +651,17 @@ int for_microbatches(mmla_ctx* c, bool od, int64_t n, F&& body) {
 // operand left the fp16 range.  f32_only: the model's weights are outside the fp16 range.
 template <class F>
 int guarded(mmla_ctx* c, bool dev, bool f32_only, F&& body) {
-  struct Restore {   // precision and flag target of the context, restored on every return
+  struct Restore {   // precision, split switch and flag targets of the context, restored on every return
     mmla_ctx* c;
     int prec;
+    bool split;
     ~Restore() {
       c->precision = prec;
+      c->lstm_split = split;
       c->range_ptr = nullptr;
+      c->timeout_ptr = nullptr;
     }
-  } restore{c, c->precision};
+  } restore{c, c->precision, c->lstm_split};
   if (f32_only) c->precision = MMLA_PREC_F32;
   if (c->precision != MMLA_PREC_F16X3) {
     c->range_ptr = nullptr;
@@ -658,26 +669,44 @@ int guarded(mmla_ctx* c, bool dev, bool f32_only, F&& body) {
   }
   if (dev) {
     c->range_ptr = c->range_dev;
+    c->timeout_ptr = c->range_dev + 3;
     return body();
   }
-  bool flagged;
-  if (c->pin_small && c->range_map) {   // the flag in host-mapped memory: no memset, no copy
-    c->range_ptr = c->range_map_dev;
-    *reinterpret_cast<volatile int*>(c->range_map) = 0;   // host calls leave the stream idle
-    CHK(body());
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    flagged = *reinterpret_cast<volatile int*>(c->range_map) != 0;
-  } else {
-    c->range_ptr = c->range_dev + 1;
-    HIPCHK(c, hipMemsetAsync(c->range_ptr, 0, sizeof(int), c->stream));
-    CHK(body());
-    HIPCHK(c, hipMemcpyAsync(c->range_host, c->range_ptr, sizeof(int), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    flagged = *c->range_host != 0;
+  // one pass of the micro-batch; -> its range flag and split-BiLSTM timeout flag
+  auto pass = [&](bool* flagged, bool* timed_out) -> int {
+    if (c->pin_small && c->range_map) {   // the flags in host-mapped memory: no memset, no copy
+      c->range_ptr = c->range_map_dev;
+      c->timeout_ptr = c->range_map_dev + 1;
+      reinterpret_cast<volatile int*>(c->range_map)[0] = 0;   // host calls leave the stream idle
+      reinterpret_cast<volatile int*>(c->range_map)[1] = 0;
+      CHK(body());
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      *flagged = reinterpret_cast<volatile int*>(c->range_map)[0] != 0;
+      *timed_out = reinterpret_cast<volatile int*>(c->range_map)[1] != 0;
+    } else {
+      c->range_ptr = c->range_dev + 1;
+      c->timeout_ptr = c->range_dev + 2;
+      HIPCHK(c, hipMemsetAsync(c->range_ptr, 0, 2 * sizeof(int), c->stream));
+      CHK(body());
+      HIPCHK(c, hipMemcpyAsync(c->range_host, c->range_ptr, 2 * sizeof(int), hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      *flagged = c->range_host[0] != 0;
+      *timed_out = c->range_host[1] != 0;
+    }
+    return MMLA_OK;
+  };
+  bool flagged = false, timed_out = false;
+  CHK(pass(&flagged, &timed_out));
+  if (timed_out) {   // a split-BiLSTM workgroup gave up waiting (NaN outputs): the unsplit kernel,
+    c->lstm_split = false;   // the same arithmetic bit for bit
+    c->lstm_split_reruns += 1;
+    CHK(pass(&flagged, &timed_out));
+    if (timed_out) return fail(c, MMLA_E_HIP, "BiLSTM timed out without the split kernel");
   }
   if (flagged) {
     c->precision = MMLA_PREC_F32;
     c->range_ptr = nullptr;
+    c->timeout_ptr = nullptr;
     c->range_reruns += 1;
     CHK(body());
   }
@@ -794,7 +823,7 @@ hipError_t lstm_run(mmla_ctx* c, const LstmW& L, const float* seq, int64_t n, in
     if (ws_get(c, S_LSTM, bilstm_h3_split_ws_bytes(), &ws) != MMLA_OK) return hipErrorOutOfMemory;
     return bilstm_h3_split_launch(seq, (int)n, T, 128, L.wth[0], L.wtl[0], L.wth[1], L.wtl[1],
                                   L.bias[0], L.bias[1], out, c->range_ptr, L.ws[0], L.ws[1], ws,
-                                  c->stream);
+                                  c->timeout_ptr, c->lstm_spin, c->stream);
   }
   if (c->precision == MMLA_PREC_F16X3 && L.wth[0])
     return bilstm_h3_launch(seq, (int)n, T, 128, L.wth[0], L.wtl[0], L.wth[1], L.wtl[1], L.bias[0],
@@ -1147,6 +1176,39 @@ extern "C" {
 
 int mmla_abi_version(void) { return MMLA_ABI_VERSION; }
 
+// CRC-32C (Castagnoli, reflected polynomial 0x82F63B78), slice-by-8 tables built once
+static uint32_t g_crc_tab[8][256];
+static void crc32c_tables() {
+  for (uint32_t i = 0; i < 256; ++i) {
+    uint32_t c = i;
+    for (int k = 0; k < 8; ++k) c = (c & 1) ? (c >> 1) ^ 0x82F63B78u : c >> 1;
+    g_crc_tab[0][i] = c;
+  }
+  for (uint32_t i = 0; i < 256; ++i)
+    for (int t = 1; t < 8; ++t) g_crc_tab[t][i] = (g_crc_tab[t - 1][i] >> 8) ^ g_crc_tab[0][g_crc_tab[t - 1][i] & 255];
+}
+
+int mmla_crc32c(const void* data, int64_t n, uint32_t* crc) {
+  if ((!data && n > 0) || n < 0 || !crc) return MMLA_E_INVALID;
+  static const bool ready = (crc32c_tables(), true);
+  (void)ready;
+  const unsigned char* p = static_cast<const unsigned char*>(data);
+  uint32_t c = 0xFFFFFFFFu;
+  int64_t i = 0;
+  for (; i + 8 <= n; i += 8) {
+    uint32_t lo, hi;
+    memcpy(&lo, p + i, 4);
+    memcpy(&hi, p + i + 4, 4);
+    lo ^= c;
+    c = g_crc_tab[7][lo & 255] ^ g_crc_tab[6][(lo >> 8) & 255] ^ g_crc_tab[5][(lo >> 16) & 255] ^
+        g_crc_tab[4][lo >> 24] ^ g_crc_tab[3][hi & 255] ^ g_crc_tab[2][(hi >> 8) & 255] ^
+        g_crc_tab[1][(hi >> 16) & 255] ^ g_crc_tab[0][hi >> 24];
+  }
+  for (; i < n; ++i) c = g_crc_tab[0][(c ^ p[i]) & 255] ^ (c >> 8);
+  *crc = c ^ 0xFFFFFFFFu;
+  return MMLA_OK;
+}
+
 int mmla_create(int device, mmla_ctx** out) {
   if (!out) return MMLA_E_INVALID;
   *out = nullptr;
@@ -1162,6 +1224,7 @@ int mmla_create(int device, mmla_ctx** out) {
   if (const char* sf = std::getenv("MMLA_NO_SIFIN")) c->sifin = std::atoi(sf) == 0;
   if (const char* ls = std::getenv("MMLA_NO_LSTM_SPLIT")) c->lstm_split = std::atoi(ls) == 0;
   if (const char* lm = std::getenv("MMLA_LSTM_SPLIT_MAX")) c->lstm_split_max = std::atoi(lm);
+  if (const char* sp = std::getenv("MMLA_DEBUG_LSTM_SPIN")) c->lstm_spin = std::atoi(sp);
   if (const char* sd = std::getenv("MMLA_NO_SIPAD")) c->si_pad_feat = std::atoi(sd) == 0;
   // a BLOCKING stream: it orders with the legacy default (NULL) stream, on which PyTorch's default
   // stream enqueues -- so a device-pointer call sees tensors a torch kernel or copy just produced
@@ -1172,9 +1235,9 @@ int mmla_create(int device, mmla_ctx** out) {
     return MMLA_E_HIP;
   }
   c->stream = c->own_stream;
-  if (hipMalloc(&c->range_dev, 2 * sizeof(int)) != hipSuccess ||
-      hipMemset(c->range_dev, 0, 2 * sizeof(int)) != hipSuccess ||
-      hipHostMalloc(&c->range_host, sizeof(int), hipHostMallocDefault) != hipSuccess) {
+  if (hipMalloc(&c->range_dev, 4 * sizeof(int)) != hipSuccess ||
+      hipMemset(c->range_dev, 0, 4 * sizeof(int)) != hipSuccess ||
+      hipHostMalloc(&c->range_host, 2 * sizeof(int), hipHostMallocDefault) != hipSuccess) {
     mmla_destroy(c);
     return MMLA_E_HIP;
   }
@@ -1189,7 +1252,7 @@ int mmla_create(int device, mmla_ctx** out) {
       mmla_destroy(c);
       return MMLA_E_HIP;
     }
-    *c->range_map = 0;
+    c->range_map[0] = c->range_map[1] = 0;
   }
   OdFeTables ot;
   od_fe_build_tables(&ot);
@@ -1385,14 +1448,28 @@ int mmla_range_check(mmla_ctx* c, int64_t* f32_reruns) {
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   if (f32_reruns) *f32_reruns = c->range_reruns;
-  int flag = 0;
+  int flag = 0, timeout = 0;
   HIPCHK(c, hipMemcpy(&flag, c->range_dev, sizeof(int), hipMemcpyDeviceToHost));
+  HIPCHK(c, hipMemcpy(&timeout, c->range_dev + 3, sizeof(int), hipMemcpyDeviceToHost));
+  if (timeout) {
+    HIPCHK(c, hipMemset(c->range_dev + 3, 0, sizeof(int)));
+    return fail(c, MMLA_E_HIP,
+                "a device-pointer call since the last check ran the split BiLSTM and one of its "
+                "workgroups timed out waiting for the others: its probabilities are NaN; re-run it");
+  }
   if (flag) {
     HIPCHK(c, hipMemset(c->range_dev, 0, sizeof(int)));
     return fail(c, MMLA_E_RANGE,
                 "a device-pointer call since the last check split an operand outside the fp16 "
                 "range (|x| >= 65504): its results are not valid; re-run it with MMLA_PREC_F32");
   }
+  return MMLA_OK;
+}
+
+int mmla_debug_counters(mmla_ctx* c, int64_t* f32_reruns, int64_t* lstm_split_reruns) {
+  if (!c) return MMLA_E_INVALID;
+  if (f32_reruns) *f32_reruns = c->range_reruns;
+  if (lstm_split_reruns) *lstm_split_reruns = c->lstm_split_reruns;
   return MMLA_OK;
 }
 

@@ -29,13 +29,14 @@ hipError_t bilstm_h3_launch(const float* seq, int n, int T, int D, const uint16_
                             float ws_fwd, float ws_bwd, hipStream_t s);
 // The same for n <= bilstm_h3_split_max_clips() with each direction's eight hidden-unit groups on
 // eight workgroups per 32 clips (h exchanged through ws between steps; bit-identical).  ws:
-// bilstm_h3_split_ws_bytes() of device memory owned by the stream; int word 63 of ws is set when a
-// workgroup gave up waiting (its outputs NaN).
+// bilstm_h3_split_ws_bytes() of device memory owned by the stream.  A workgroup that gave up waiting
+// for the others (after `spin` polls; <= 0: the default bound) writes NaN for its units and sets int
+// word 63 of ws and *timeout_flag (nullable): the caller must not use that launch's outputs.
 hipError_t bilstm_h3_split_launch(const float* seq, int n, int T, int D, const uint16_t* wfh,
                                   const uint16_t* wfl, const uint16_t* wbh, const uint16_t* wbl,
                                   const float* bias_fwd, const float* bias_bwd, float* out,
                                   int* range_flag, float ws_fwd, float ws_bwd, void* ws,
-                                  hipStream_t s);
+                                  int* timeout_flag, int spin, hipStream_t s);
 size_t bilstm_h3_split_ws_bytes();
 int bilstm_h3_split_max_clips();
 // split at the direction's power-of-two weight scale ws (the kernel's ws_fwd / ws_bwd)

@@ -477,8 +477,15 @@ __global__ void __launch_bounds__(512, (LSTM_W4 && MT == 1) ? 4 : 2) bilstm_h3_k
 // 8 (s + 1) (acquire) before reading all 256 columns.  Outputs are bit-identical to
 // bilstm_h3_kernel (tests/test_gpu_batching.py).  Batches of up to 8 x 32 clips: one 32-row tile per
 // grid z, with its own counters sync[2 tile + dir] (zero at launch: bilstm_h3_split_launch clears them
-// on the stream) and exchange buffers.  Waits are bounded at LSTM_SPLIT_SPIN polls: a workgroup that
-// gives up sets sync[63], writes NaN for its units and exits, so the grid always drains.
+// on the stream) and exchange buffers.  Waits are bounded at `spin` polls (LSTM_SPLIT_SPIN unless a
+// debug limit is given): thread 0 polls and the decision is broadcast through LDS, so a workgroup gives
+// up as a whole -- it sets sync[63] and *timeout_flag, writes NaN for its units and exits, and the grid
+// always drains.  The host reads the flag (capi.cpp guarded(): a host call re-runs the micro-batch on
+// bilstm_h3_kernel, bit-identical; a device-pointer call reports MMLA_E_HIP at mmla_synchronize).
+// Publication: each wave's h stores, its agent-scope release fence, the workgroup barrier, then
+// thread 0's counter increment as an agent-scope RELEASE read-modify-write; the reader's thread 0
+// observes the count, the barrier hands that on, and every wave fences acquire at agent scope before
+// it reads the exchange buffer.
 constexpr int LSTM_SPLIT_ROWS = 32;
 constexpr int LSTM_SPLIT_SPIN = 1 << 22;
 // up to 8 row tiles of 32 clips (grid z): at most 128 workgroups, so all of them are resident at once
@@ -495,7 +502,8 @@ __global__ void __launch_bounds__(256, 1) bilstm_h3_split_kernel(const float* __
                                                                  float* __restrict__ out,
                                                                  int* __restrict__ range_flag,
                                                                  float ws_f, float ws_b, int* sync,
-                                                                 _Float16* xbuf) {
+                                                                 _Float16* xbuf, int* timeout_flag,
+                                                                 int spin) {
   constexpr int K = LSTM_U + D;
   constexpr int KST = K / 16;
   constexpr int LDA = K + 8;
@@ -505,6 +513,7 @@ __global__ void __launch_bounds__(256, 1) bilstm_h3_split_kernel(const float* __
   __shared__ __attribute__((aligned(16))) _Float16 Ahi[ROWS * LDA];
   __shared__ __attribute__((aligned(16))) _Float16 Alo[ROWS * LDA];
   __shared__ float G[4][16][64];   // the four gates' accumulators, [gate][register][lane]
+  __shared__ int arrived;          // thread 0's wait result, the same for the whole workgroup
   const int tid = threadIdx.x, lane = tid & 63, gate = tid >> 6;
   const int grp = blockIdx.x;   // hidden units [32 grp, 32 grp + 32) (bilstm_h3_kernel's wave grp)
   const int dir = blockIdx.y;
@@ -567,12 +576,17 @@ __global__ void __launch_bounds__(256, 1) bilstm_h3_split_kernel(const float* __
   bool dead = false;
   for (int s = 0; s < T; ++s) {
     if (s > 0) {   // every workgroup's h_{t-1} published
-      int it = 0;
-      while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < 8 * s) {
-        __builtin_amdgcn_s_sleep(1);
-        if (++it == LSTM_SPLIT_SPIN) break;
+      if (tid == 0) {
+        int it = 0;
+        while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < 8 * s && it < spin) {
+          __builtin_amdgcn_s_sleep(1);
+          ++it;
+        }
+        arrived = it < spin || __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= 8 * s;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // pairs with the publishers' release RMW
       }
-      if (it == LSTM_SPLIT_SPIN) {
+      __syncthreads();
+      if (!arrived) {   // workgroup-uniform: no wave is left at a barrier the others skip
         dead = true;
         break;
       }
@@ -629,12 +643,15 @@ __global__ void __launch_bounds__(256, 1) bilstm_h3_split_kernel(const float* __
       static_assert(2 * ROWS * 4 == NTH, "one publish chunk per thread");
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");   // each wave: its stores, then L2 written back
       __syncthreads();
-      if (tid == 0) __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (tid == 0) __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
       stage_x(dir == 0 ? s + 1 : T - 2 - s);   // under the other workgroups' arrival
     }
   }
   if (dead) {
-    if (tid == 0) __hip_atomic_store(sync + 63, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0) {
+      __hip_atomic_store(sync + 63, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (timeout_flag) *timeout_flag = 1;
+    }
     for (int j = 0; j < 4; ++j) {
       const int r = 4 * gate + j, row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
       if (row < nr) out[(int64_t)row * 512 + dir * LSTM_U + col] = __builtin_nanf("");
@@ -820,16 +837,18 @@ int bilstm_h3_split_max_clips() { return LSTM_SPLIT_TILES * LSTM_SPLIT_ROWS; }
 hipError_t bilstm_h3_split_launch(const float* seq, int n, int T, int D, const uint16_t* wfh,
                                   const uint16_t* wfl, const uint16_t* wbh, const uint16_t* wbl,
                                   const float* bf, const float* bb, float* out, int* range_flag,
-                                  float ws_fwd, float ws_bwd, void* ws, hipStream_t s) {
+                                  float ws_fwd, float ws_bwd, void* ws, int* timeout_flag,
+                                  int spin, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   if (D != 128 || n > LSTM_SPLIT_TILES * LSTM_SPLIT_ROWS || T < 1) return hipErrorInvalidValue;
+  if (spin <= 0) spin = LSTM_SPLIT_SPIN;
   const int tiles = (n + LSTM_SPLIT_ROWS - 1) / LSTM_SPLIT_ROWS;
   int* sync = static_cast<int*>(ws);
   _Float16* xbuf = reinterpret_cast<_Float16*>(static_cast<char*>(ws) + 256);
   const hipError_t e = hipMemsetAsync(sync, 0, 64 * sizeof(int), s);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL((bilstm_h3_split_kernel<128>), dim3(8, 2, tiles), dim3(256), 0, s, seq, n, T, wfh, wfl,
-                     wbh, wbl, bf, bb, out, range_flag, ws_fwd, ws_bwd, sync, xbuf);
+                     wbh, wbl, bf, bb, out, range_flag, ws_fwd, ws_bwd, sync, xbuf, timeout_flag, spin);
   return hipGetLastError();
 }
 

@@ -19,13 +19,21 @@ import numpy as np
 from . import _lib, tfbundle, weights
 
 
-def _kind_from_path(path):
+def _layout_from_path(path):
+    """(kind, n_classes, head) from the bundle index (tfbundle.layout), or None without one"""
     idx = os.path.join(path, 'variables', 'variables.index')
     if os.path.exists(idx):
-        shapes = tfbundle.variable_shapes(idx)
-        k0 = shapes.get('layer_with_weights-0/kernel')
-        if k0 is not None:
-            return weights.OD if len(k0) == 4 else weights.SI
+        try:
+            return tfbundle.layout(tfbundle.variable_shapes(idx))[:3]
+        except ValueError:
+            return None
+    return None
+
+
+def _kind_from_path(path):
+    lay = _layout_from_path(path)
+    if lay is not None:
+        return lay[0]
     low = path.replace('\\', '/').lower()
     return weights.OD if 'overlap' in low or 'timit2' in low or 'timit1' in low else weights.SI
 
@@ -95,14 +103,22 @@ class SpeakerIdModel(_Model):
 
 def load_model(path, kind=None, n_classes=None, head=None, seed=0, device=None,
                allow_synthetic=False):
-    """tf.keras.models.load_model drop-in for the two reference model directories.  Raises
-    FileNotFoundError when the trained variables are absent, unless allow_synthetic=True."""
-    kind = _kind_from_path(path) if kind is None else kind
+    """tf.keras.models.load_model drop-in for the reference's model directories: the OD base models
+    (timit/models/timit{1.0,2.0}), the SI base model (timit/model, Dense(630) softmax) and the
+    deployed SI model transfer_learning saves (experiment/model: the sliced base nested inside a
+    model with the customized_dense sigmoid head, speaker_identification.py:401-410,456) -- the
+    layout is read from the bundle index (tfbundle.layout), K and the head from its head kernel.
+    Raises FileNotFoundError when the trained variables are absent, unless allow_synthetic=True."""
+    lay = _layout_from_path(path)
+    kind = (lay[0] if lay else _kind_from_path(path)) if kind is None else kind
     synthetic = False
     try:
-        W = tfbundle.load_bundle(path, 40 if kind == weights.OD else 41)
+        W, (bkind, bk, bhead) = tfbundle.load_bundle(path, with_layout=True)
+        if bkind != kind:
+            raise ValueError(f'{path}: bundle holds a {"OD" if bkind == weights.OD else "SI"} model')
         if kind == weights.SI:
-            n_classes = W['layer_with_weights-42/kernel'].shape[1]
+            n_classes = bk
+            head = bhead if head is None else head
     except (FileNotFoundError, OSError) as e:
         if not allow_synthetic:
             raise FileNotFoundError(

@@ -155,7 +155,7 @@ def _vad_owner(ctx, owner, mode):
     the record_on_pc modules); a context holds one detector: (re)create it when another script's
     detector or another mode was in use, else keep its adaptive state"""
     if getattr(ctx, 'vad_owner', None) != (owner, mode) or getattr(ctx, 'vad_streams', None) != 1:
-        ctx.vad_reset(1, mode)
+        ctx.vad_reset(1, mode)   # clears ctx.vad_owner (any other reset clears it too)
         ctx.vad_owner = (owner, mode)
 
 

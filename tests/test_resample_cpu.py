@@ -84,3 +84,16 @@ def test_resampler_restatement_on_tones(sr0, sr1):
     t1 = np.arange(len(y)) / sr1
     ref = sum(0.2 * np.sin(2 * np.pi * fk * t1) for fk in f)
     assert np.abs(y[400:-400] - ref[400:-400]).max() < (2e-6 if sr1 > sr0 else 1e-3)
+
+
+def test_rms_long_full_scale_matches_audioop():
+    """audioop.rms sums x*x in a float64 running sum, sample by sample; past 2^53 (~8.4 M
+    full-scale samples) that sum rounds, so an exact integer sum gives a different (unsigned) rms
+    for a long constant signal (32767 vs audioop's 32766 at 12 M samples)."""
+    from mmla_audio_amd.audio_segment import AudioSegment
+    for v, n in ((32767, 12_000_000), (30001, 16_000_000), (-32768, 9_000_000)):
+        x = np.full(n, v, np.int16)
+        assert AudioSegment(x, 16000).rms == audioop.rms(x.tobytes(), 2), (v, n)
+    rng = np.random.default_rng(5)
+    x = _pcm(rng, 10_000_000)
+    assert AudioSegment(x, 16000).rms == audioop.rms(x.tobytes(), 2)
