@@ -73,9 +73,17 @@ def parse():
     ap.add_argument('--microbatch', type=int, default=0,
                     help='clips per internal micro-batch (0 = the library default)')
     ap.add_argument('--cpu-seconds', type=float, default=20.0)
+    ap.add_argument('--classes', type=int, default=630,
+                    help='si_pipeline: speakers K of the Dense head (630 = the base model; SURVEY 8(d) '
+                         'config 4 also asks for K = 8 with the deployed sigmoid head)')
+    ap.add_argument('--head', choices=['softmax', 'sigmoid'], default=None,
+                    help='si_pipeline head (default: softmax for K = 630, sigmoid otherwise -- '
+                         'transfer_learning\'s customized_dense, speaker_identification.py:409)')
     args = ap.parse_args()
     if args.steps is None:
         args.steps = 50 if args.workload == 'od_features' else 3
+    if args.head is None:
+        args.head = 'softmax' if args.classes == 630 else 'sigmoid'
     return args
 
 
@@ -181,7 +189,7 @@ def fe_sample_indices(n, grid, k=24, seed=20261015):
     return sorted(i for i in idx if 0 <= i < n)
 
 
-def parity_sample(ctx, wl, pcm, probs, argmax, W, mb, clip_len, k=24, fe_out=None):
+def parity_sample(ctx, wl, pcm, probs, argmax, W, mb, clip_len, k=24, fe_out=None, head='softmax'):
     """oracle (float64) vs the timed run's outputs on clips spread across the whole batch"""
     from oracle import od_fe, si_fe
     from oracle.nets_torch import Nets
@@ -245,7 +253,7 @@ def parity_sample(ctx, wl, pcm, probs, argmax, W, mb, clip_len, k=24, fe_out=Non
         torch.cuda.synchronize()
         xs = np.stack([si_fe.input_feature_gen(host[j])[0] for j in range(len(idx))])
         out['si_feature_max_abs_err'] = float(np.abs(feat.cpu().numpy() - xs).max())
-        ref = Nets(W).si_forward(xs.astype(np.float32))
+        ref = Nets(W).si_forward(xs.astype(np.float32), head=head)
     if wl in ('od_pipeline', 'si_pipeline'):
         from oracle import compare
         gp = probs[idx].cpu().numpy()
@@ -307,8 +315,9 @@ def main():
         W = weights.synthetic(weights.OD, seed=0)
         ctx.load_weights(weights.OD, weights.pack(weights.OD, W), 2)
     if wl == 'si_pipeline':
-        W = weights.synthetic(weights.SI, seed=0, n_classes=630)
-        ctx.load_weights(weights.SI, weights.pack(weights.SI, W, 630), 630, _lib.HEAD_SOFTMAX)
+        W = weights.synthetic(weights.SI, seed=0, n_classes=args.classes)
+        ctx.load_weights(weights.SI, weights.pack(weights.SI, W, args.classes), args.classes,
+                         _lib.HEAD_SOFTMAX if args.head == 'softmax' else _lib.HEAD_SIGMOID)
     mb_od, mb_si = ctx.get_microbatch()
     mb = {'od_pipeline': mb_od, 'si_pipeline': mb_si}.get(wl, clips)
 
@@ -322,7 +331,7 @@ def main():
         noise_clip = (0.01 * torch.randn(160000, generator=gen, device='cuda')).cpu().numpy()
         ctx.nr_set_noise(noise_clip)
         nr_out = torch.empty_like(yf)
-    K = 2 if wl == 'od_pipeline' else 630
+    K = 2 if wl == 'od_pipeline' else args.classes
     probs = torch.empty((clips, K), dtype=torch.float32, device='cuda')
     argmax = torch.empty(clips, dtype=torch.int32, device='cuda')
     norm = torch.empty((clips, 128, 151), dtype=torch.float32, device='cuda') if wl == 'od_features' else None
@@ -425,7 +434,7 @@ def main():
             parity = {'sample_clips': len(idx), 'nr_max_abs_err_vs_oracle': err}
         else:
             parity = parity_sample(ctx, wl, pcm, probs, argmax, W, mb, clip_len,
-                                   fe_out=(norm, zcr) if wl == 'od_features' else None)
+                                   fe_out=(norm, zcr) if wl == 'od_features' else None, head=args.head)
 
     # batch-1 latency of the host-pointer call the reference's real-time loop makes (one 2.56 s
     # window per predict, record_on_pc.py:139-160): median of 20 after 5 warmups, outside the
@@ -449,7 +458,7 @@ def main():
             'od_pipeline': 'config 3: fused log-mel/ZCR front-end -> uint8 image -> OD-NET ResLSTM '
                            '-> softmax, per GPU',
             'si_pipeline': 'config 4: MFCC+d+dd (float64) -> SI-NET Conv1D ResNet+BiLSTM -> '
-                           'Dense(630) softmax, per GPU',
+                           f'Dense({args.classes}) {args.head}, per GPU',
             'od_features': 'config 2: OD front-end kernel only (log-mel norm + ZCR out)',
             'noise_gate': 'SURVEY 8f row 3: nr.reduce_noise(stationary=True) gate on 2.5 s clips '
                           '(noisereduce 2.0 defaults, float64 STFT), per GPU',
@@ -469,6 +478,7 @@ def main():
                       ' (int16); seeded synthetic weights in the reference variables.index layout '
                       '(trained blobs absent)')),
             'config': {'workload': f'{wl} ({desc})', 'clips_per_gpu': clips,
+                       **({'classes': args.classes, 'head': args.head} if wl == 'si_pipeline' else {}),
                        'global_batch': world * clips, 'clip_samples': clip_len, 'microbatch': mb,
                        'parallelism': f'dp{world}' + ('+rccl_allgather_logits' if world > 1 and pipeline else '')},
             'world_size': world, 'gpus_requested': args.gpus, 'rank_devices': devices,

@@ -144,7 +144,9 @@ int mmla_load_weights(mmla_ctx* ctx, int model_kind, const float* packed, int64_
 int mmla_od_features(mmla_ctx* ctx, const int16_t* pcm, int64_t n_clips, int64_t clip_stride,
                      const int32_t* lens, int32_t clip_len, float* db, float* norm_db, float* zcr,
                      uint8_t* img, uint32_t flags);
-/* Same on float PCM in librosa.load's scale (y = x / 32768 for 16-bit files; any value): the
+/* Same on float PCM in librosa.load's scale (y = x / 32768 for 16-bit files; |y| < 8188, since y 2^3 is
+ * split into fp16 hi + lo -- a host call with a larger or non-finite sample in the read window returns
+ * MMLA_E_RANGE, a device-pointer call reports it from the next mmla_range_check / mmla_synchronize): the
  * drop-in's path for what librosa.load(path, sr=None, mono=True) returns from a WAV that is not
  * 16-bit mono (stereo downmixed by the channel mean, 8/24/32-bit and float files) --
  * overlap_features_generator.py:72,93.  Zero crossings treat |y| <= 1e-10 as 0, as librosa. */

@@ -24,6 +24,7 @@
 #include "vad.h"
 #include "resample.h"
 #include "siu.h"
+#include "odu.h"
 
 namespace {
 
@@ -136,6 +137,9 @@ struct mmla_ctx {
   bool sifin = true;
   // fused SI pipeline: si_fe writes 40-float feature rows for the stem (env MMLA_NO_SIPAD=1: 39)
   bool si_pad_feat = true;
+  // OD blocks 4-9 as one fused kernel each (odu.hip: t1 on chip); env MMLA_NO_ODU=1 at create: the
+  // conv_h3 pairs (A/B, bit-identical)
+  bool odu = false;   // (default on once validated on the GPU)
   // batches of <= lstm_split_max clips: the 3xFP16 BiLSTM with each direction's hidden units on eight workgroups
   // (nets.hip bilstm_h3_split_kernel); env MMLA_NO_LSTM_SPLIT=1 at create: one workgroup per direction
   bool lstm_split = true;
@@ -928,6 +932,51 @@ int run_od_net(mmla_ctx* c, const uint8_t* img_u8, const float* img_f32, int64_t
       }
       continue;
     }
+    if (c->odu && c->precision == MMLA_PREC_F16X3 && B.c3.wh && B.c4.wh && (!POOL[b] || B.sc.wh) &&
+        odu_supported(h, w, B.c3.cin, B.c3.cout, POOL[b]) && B.c3.cin_pad == B.c3.cin &&
+        B.c3.cout_pad == B.c3.cout && B.c4.cin == B.c3.cout && B.c4.cout == B.c3.cout &&
+        B.c4.cin_pad == B.c4.cin && B.c4.cout_pad == B.c4.cout && B.c4.kh == 4 && B.c4.kw == 1 &&
+        (!POOL[b] || (B.sc.cin == B.c3.cin && B.sc.cout == B.c3.cout && B.sc.cout_pad == B.sc.cout))) {
+      // the whole block in one launch: t1 stays in LDS (odu.hip), bit-identical to the pair below
+      OduArgs o{};
+      o.x = X;
+      o.y = T1;
+      o.wah = B.c3.wh;
+      o.wal = B.c3.wl;
+      o.wbh = B.c4.wh;
+      o.wbl = B.c4.wl;
+      o.ba = B.c3.bias;
+      o.bb = B.c4.bias;
+      o.s_in = B.bn_in.scale;
+      o.t_in = B.bn_in.shift;
+      o.s_mid = B.bn_mid.scale;
+      o.t_mid = B.bn_mid.shift;
+      o.ua = B.c3.unscale();
+      o.ub = B.c4.unscale();
+      o.n = (int)n;
+      o.range_flag = c->range_ptr;
+      if (POOL[b]) {
+        o.wsh = B.sc.wh;
+        o.wsl = B.sc.wl;
+        o.bs = B.sc.bias;
+        o.us = B.sc.unscale();
+      }
+      LAUNCH(c, MMLA_STAGE_CONV,
+             2.0 * n * h * w * (9.0 * B.c3.cin * B.c3.cout + 4.0 * B.c4.cin * B.c4.cout) +
+                 (POOL[b] ? 2.0 * n * (h / 2) * (w / 2) * B.sc.cin * B.sc.cout : 0.0),
+             odu_launch(o, h, w, B.c3.cin, B.c3.cout, POOL[b], c->stream));
+      if (POOL[b]) {
+        h /= 2;
+        w /= 2;
+      }
+      std::swap(X, T1);
+      if (stop == b + 1) {
+        *tap = X;
+        *tap_n = n * h * w * CH[b];
+        return MMLA_OK;
+      }
+      continue;
+    }
     CHK(conv_spatial(c, B.c3, X, T1, (int)n, h, w, &B.bn_in, PRO_BN_ELU, EPI_BIAS, nullptr));
     if (POOL[b]) {
       if (c->precision == MMLA_PREC_F16X3) {
@@ -1226,6 +1275,7 @@ int mmla_create(int device, mmla_ctx** out) {
   if (const char* lm = std::getenv("MMLA_LSTM_SPLIT_MAX")) c->lstm_split_max = std::atoi(lm);
   if (const char* sp = std::getenv("MMLA_DEBUG_LSTM_SPIN")) c->lstm_spin = std::atoi(sp);
   if (const char* sd = std::getenv("MMLA_NO_SIPAD")) c->si_pad_feat = std::atoi(sd) == 0;
+  if (const char* ou = std::getenv("MMLA_NO_ODU")) c->odu = std::atoi(ou) == 0;
   // a BLOCKING stream: it orders with the legacy default (NULL) stream, on which PyTorch's default
   // stream enqueues -- so a device-pointer call sees tensors a torch kernel or copy just produced
   // without an explicit synchronisation (a non-blocking stream raced them: a 65 536-clip call read
@@ -1590,12 +1640,31 @@ static int od_features_common(mmla_ctx* c, const T* pcm, int64_t n, int64_t stri
     return fail(c, MMLA_E_INVALID, "float PCM needs the MFMA front-end (unset MMLA_OD_FE_V2)");
   HIPCHK(c, hipSetDevice(c->device));
   const bool dev = flags & MMLA_DEVICE_PTR;
+  if constexpr (std::is_same<T, float>::value) {
+    // the front-end splits y 2^3 into fp16 hi + lo: host samples are checked here (what the kernel
+    // reads: the first min(len, 24000) of each clip); device buffers by the kernel into the sticky
+    // range word (mmla_range_check / mmla_synchronize report it)
+    if (!dev && pcm) {
+      for (int64_t i = 0; i < n; ++i) {
+        const int64_t len = std::min<int64_t>(lens ? lens[i] : clip_len, MMLA_OD_CLIP);
+        for (int64_t j = 0; j < len; ++j)
+          if (!(std::fabs(pcm[i * stride + j]) < 8188.0f))
+            return fail(c, MMLA_E_RANGE,
+                        "float PCM clip %lld sample %lld = %g: the front-end needs |y| < 8188 (y * 8 is "
+                        "split into fp16)", (long long)i, (long long)j, (double)pcm[i * stride + j]);
+      }
+    }
+  }
   auto body = [&](int64_t c0, int64_t cnt) -> int {
     PcmT<T> p;
     CHK(stage_pcm(c, pcm, c0, cnt, stride, lens, clip_len, MMLA_OD_CLIP, dev, &p));
     OdFeArgs a{};
-    if constexpr (std::is_same<T, float>::value) a.pcm_f32 = p.p;
-    else a.pcm = p.p;
+    if constexpr (std::is_same<T, float>::value) {
+      a.pcm_f32 = p.p;
+      a.range_flag = dev ? c->range_dev : nullptr;
+    } else {
+      a.pcm = p.p;
+    }
     a.clip_stride = p.stride;
     a.lens = p.lens;
     a.clip_len = p.clip_len;

@@ -43,6 +43,8 @@ struct OdFeArgs {
   float* zcr;               // [n,151]     nullable
   uint8_t* img;             // [n,128,151,3] nullable
   float* scratch;           // [n,151,128] mel-power scratch (frame-major): v2 only
+  int* range_flag;          // nullable: set when a float PCM sample is outside the split range
+                            // (|y| >= 8188 or not finite: y 2^3 must fit fp16)
 };
 
 void od_fe_build_tables(OdFeTables* t);

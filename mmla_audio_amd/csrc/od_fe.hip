@@ -924,6 +924,10 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
     nx[3] = v.w;
   };
 
+  // float PCM: y 2^3 is split into fp16 hi + lo, so |y| must stay below 65504 / 8 (a larger or
+  // non-finite sample sets a.range_flag: the host call reports MMLA_E_RANGE)
+  constexpr float F32_PCM_RANGE = 8188.0f;
+  bool fbad = false;
   // ---- staging of (clip, t): chunk c holds p = 8c .. 8c + 7 (reflect-padded, zero past len), split
   //      x' = x 2^-12 into fp16 hi + lo, transposed store T[p & 15][p >> 4] = (hi, lo) ---------------
   auto stage = [&](int64_t clip, auto T_) {
@@ -945,6 +949,7 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
         const bool in = live && i >= 0 && i < ci.len;
         if (a.pcm_f32) {
           const float y = in ? a.pcm_f32[clip * a.clip_stride + i] : 0.0f;
+          fbad |= !(fabsf(y) < F32_PCM_RANGE);
           d[j] = split1(y * (32768.0f * X_SCALE));
           sg |= (uint32_t)(y < -1e-10f) << j;
         } else {
@@ -1386,6 +1391,7 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
       FE3_MARK(3);
     }, std::make_integer_sequence<int, NTILE>{});
   }
+  if (fbad && a.range_flag) *a.range_flag = 1;
 }
 
 }  // namespace v3

@@ -136,3 +136,38 @@ def test_si_lstm_input_overflow_host_call_reruns_in_f32():
     ref = _ctx(W_si=W, prec=_lib.PREC_F32)
     p32, a32, _ = ref.si_pipeline(pcm)
     assert np.array_equal(p, p32) and np.array_equal(a, a32)
+
+
+def test_float_pcm_outside_split_range():
+    """the float-PCM front-end splits y 2^3 into fp16, so |y| must stay below 8188.
+    A host call with a larger (or non-finite) sample in the 24 000-sample window returns MMLA_E_RANGE
+    instead of an overflowed image; one outside the window is never read and passes; a device-pointer
+    call reports it from mmla_synchronize.  In-range loud float audio (|y| up to 8000) is exact."""
+    import torch
+    from mmla_audio_amd import _lib
+    c = _ctx()
+    y = (synth.clip(7, 30000).astype(np.float32) / 32768.0)
+    loud = y * 8000.0 / np.abs(y).max()
+    f = c.od_features(loud[None])
+    assert np.isfinite(f['db']).all()
+    bad = loud.copy()
+    bad[1234] = 9000.0
+    with pytest.raises(_lib.MmlaError) as e:
+        c.od_features(bad[None])
+    assert e.value.code == _lib.MMLA_E_RANGE
+    nan = loud.copy()
+    nan[10] = np.nan
+    with pytest.raises(_lib.MmlaError):
+        c.od_features(nan[None])
+    late = loud.copy()
+    late[25000] = 9000.0           # past the 24 000 samples the front-end reads
+    c.od_features(late[None])
+    dev = torch.from_numpy(bad[None]).cuda()
+    out = torch.empty((1, 128, 151), dtype=torch.float32, device='cuda')
+    c.set_stream(torch.cuda.current_stream().cuda_stream)
+    c._check(c.lib.mmla_od_features_f32(c.h, dev.data_ptr(), 1, 30000, None, 30000, None, out.data_ptr(),
+                                        None, None, _lib.MMLA_DEVICE_PTR), 'f32 dev')
+    with pytest.raises(_lib.MmlaError) as e:
+        c.synchronize()
+    assert e.value.code == _lib.MMLA_E_RANGE
+    c.synchronize()
