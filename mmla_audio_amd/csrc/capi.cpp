@@ -139,7 +139,7 @@ struct mmla_ctx {
   bool si_pad_feat = true;
   // OD blocks 4-9 as one fused kernel each (odu.hip: t1 on chip); env MMLA_NO_ODU=1 at create: the
   // conv_h3 pairs (A/B, bit-identical)
-  bool odu = false;   // (default on once validated on the GPU)
+  bool odu = true;
   // batches of <= lstm_split_max clips: the 3xFP16 BiLSTM with each direction's hidden units on eight workgroups
   // (nets.hip bilstm_h3_split_kernel); env MMLA_NO_LSTM_SPLIT=1 at create: one workgroup per direction
   bool lstm_split = true;
