@@ -79,13 +79,13 @@ MMLA_DEV bool in_range4(float4 v) {
 // H x W image, CIN -> C channels, strips of TW columns, 4 waves: WN = C / 32 waves along the output
 // channels (one 32-channel tile each, so no weight fragment is fetched twice per workgroup), WM along
 // the strip's H * TW pixels, MT 32-pixel tiles per wave
-template <int H, int W, int CIN, int C, int TW, bool POOL>
-__global__ void __launch_bounds__(256, 2) odu_kernel(OduArgs a) {
-  constexpr int NT = 256;
-  constexpr int WN = C / 32, WM = 4 / WN;
+template <int H, int W, int CIN, int C, int TW, bool POOL, int NW, int MINW>
+__global__ void __launch_bounds__(64 * NW, MINW) odu_kernel(OduArgs a) {
+  constexpr int NT = 64 * NW;
+  constexpr int WN = C / 32, WM = NW / WN;
   constexpr int M = H * TW;
   constexpr int MT = M / (WM * 32);
-  static_assert(MT * WM * 32 == M && WN * WM == 4, "tiling");
+  static_assert(MT * WM * 32 == M && WN * WM == NW, "tiling");
   static_assert(!POOL || (TW == 2 && H % 2 == 0 && W % 2 == 0 && MT <= 4), "pool strips");
   static_assert(POOL || CIN == C, "residual blocks keep their width");
   constexpr int TLW = (W + TW - 1) / TW;
@@ -389,11 +389,11 @@ __global__ void __launch_bounds__(256, 2) odu_kernel(OduArgs a) {
   if (rbad && a.range_flag) *a.range_flag = 1;
 }
 
-template <int H, int W, int CIN, int C, int TW, bool POOL>
+template <int H, int W, int CIN, int C, int TW, bool POOL, int NW = 4, int MINW = 2>
 hipError_t launch(const OduArgs& a, hipStream_t s) {
   constexpr int TLW = (W + TW - 1) / TW;
   const int64_t blocks = (int64_t)a.n * TLW;
-  hipLaunchKernelGGL((odu_kernel<H, W, CIN, C, TW, POOL>), dim3((unsigned)blocks), dim3(256), 0, s, a);
+  hipLaunchKernelGGL((odu_kernel<H, W, CIN, C, TW, POOL, NW, MINW>), dim3((unsigned)blocks), dim3(64 * NW), 0, s, a);
   return hipGetLastError();
 }
 
@@ -411,8 +411,12 @@ hipError_t odu_launch(const OduArgs& a, int h, int w, int cin, int c, bool pool,
   if (!a.x || !a.y || a.x == a.y || !odu_supported(h, w, cin, c, pool) ||
       (pool && (!a.wsh || !a.wsl || !a.bs)))
     return hipErrorInvalidValue;
+  // strips and register budgets, measured per kernel (rocprof, one box, per 16 384-clip launch):
+  // blocks 5-6 TW 4 at 3 waves per SIMD (<= 168 VGPRs, 1 spilled) 8.56 -> 7.55 ms; TW 2 with two-wave
+  // workgroups 8.16 ms; 4 waves per SIMD (<= 128 VGPRs) spill 20-44 VGPRs: block 7 15.5 -> 17.2 ms,
+  // blocks 5-6 10.6 ms.  Blocks 4 and 8-9 are LDS-bound at 3 workgroups per CU (42 / 41 KB)
   if (h == 64 && pool) return launch<64, 76, 32, 64, 2, true>(a, s);
-  if (h == 32 && c == 64) return launch<32, 38, 64, 64, 4, false>(a, s);
+  if (h == 32 && c == 64) return launch<32, 38, 64, 64, 4, false, 4, 3>(a, s);
   if (h == 32 && pool) return launch<32, 38, 64, 128, 2, true>(a, s);
   return launch<16, 19, 128, 128, 4, false>(a, s);
 }
