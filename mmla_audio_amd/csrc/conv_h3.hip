@@ -33,16 +33,6 @@
 
 #include <cstring>
 
-#ifndef CH_EXP
-#define CH_EXP 0   // 1: s_memtime phase timeline of one selected launch (dev build, tools/ch_timeline.py)
-#endif
-#if CH_EXP
-// selection (kh, kw, h, cin, cout) and per-(workgroup, wave) phase sums of the first 8192
-// workgroups of blockIdx.y == 0: [prologue, stage, barrier, taps, epilogue, total, chunks, 0]
-__device__ int g_ch_sel[5];
-__device__ unsigned long long g_ch_t[8192 * 4 * 8];
-#define CH_T() __builtin_amdgcn_s_memtime()
-#endif
 
 namespace {
 
@@ -56,11 +46,8 @@ constexpr float ACT_SCALE = 16.0f;      // 2^4: staged activations
 // weights are split at a per-tensor power-of-two scale (conv_h3_split_weights, capi.cpp pick_wscale:
 // 2^8 for the usual |w| in [1/16, 255.9)); the epilogue multiplies by a.unscale = 2^-4 / that scale
 constexpr float ACT_RANGE = 65504.0f / ACT_SCALE;   // largest finite fp16 / the activation scale
-// CONV_H3_BUFB: the B fragments by raw buffer loads from a wave-uniform descriptor (voffset = the
+// The B fragments by raw buffer loads from a wave-uniform descriptor (voffset = the
 // lane's 32-bit offset, soffset = the uniform (tap, k-step) offset): no per-load 64-bit address VALU
-#ifndef CONV_H3_BUFB
-#define CONV_H3_BUFB 1
-#endif
 MMLA_DEV __amdgpu_buffer_rsrc_t h3_rsrc(const void* p) {
   const uint64_t u = reinterpret_cast<uint64_t>(p);
   const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)u);
@@ -70,14 +57,9 @@ MMLA_DEV __amdgpu_buffer_rsrc_t h3_rsrc(const void* p) {
 }
 // 16 B of a split weight at half index uoff (wave-uniform) + lofs (this lane's)
 MMLA_DEV f16x8 h3_frag(const uint16_t* base, __amdgpu_buffer_rsrc_t r, size_t uoff, int lofs) {
-#if CONV_H3_BUFB
   (void)base;
   return __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(r, (uint32_t)lofs * 2u,
                                                                          (int)(uoff * 2), 0));
-#else
-  (void)r;
-  return *reinterpret_cast<const f16x8*>(base + uoff + lofs);
-#endif
 }
 
 
@@ -101,11 +83,8 @@ template <int KH, int BN, int TW>
 // the SI Conv1D layers with BN <= 64 (K = 3 x 32 or 3 x 64: little work per row) take 256-row tiles:
 // the per-tile fixed costs (B fragments, bias, setup) over twice the rows -- SI conv 41.05 -> 40.51 ms
 // per 3 steps, outputs bit-identical (A/B, round 4)
-#ifndef CONV_SI_ROWS
-#define CONV_SI_ROWS 256
-#endif
 constexpr int tile_px() {
-  return BN == 64 && TW > 1 && !(KH == 3 && TW == 16) ? 256 : (TW == 1 && BN <= 64 ? CONV_SI_ROWS : BM);
+  return BN == 64 && TW > 1 && !(KH == 3 && TW == 16) ? 256 : (TW == 1 && BN <= 64 ? 256 : BM);
 }
 
 // TW == 0 (LIN): a tile is 128 consecutive pixels of the whole batch in NHWC order (rows of all
@@ -148,17 +127,11 @@ template <class S> MMLA_DEV constexpr int shp_co() { return ShapeOf<S>::co; }
 // 64-channel residual conv(4,1) of OD blocks 5-6 (172 -> 166 VGPRs, 44.8 KB LDS: 3 workgroups per
 // CU); conv -0.4 % (OD) / -0.5 % (SI) per step in an A/B.  2 elsewhere: forced to 3, the block-4
 // conv(4,1) + pool and the 19-wide BN 128 layers spill 64-152 B per lane.
-#ifndef CONV_MINW_SI
-#define CONV_MINW_SI 3
-#endif
-#ifndef CONV_MINW_R64
-#define CONV_MINW_R64 3
-#endif
 template <int KH, int BN, int TW, int EPI, bool FIXED>
 constexpr int conv_minw() {
   return EPI == EPI_ADD_SC                                            ? 2
-         : TW == 1 && BN == 128                                       ? CONV_MINW_SI
-         : (FIXED && KH == 4 && BN == 64 && TW == 8 && EPI == EPI_ADD) ? CONV_MINW_R64
+         : TW == 1 && BN == 128                                       ? 3
+         : (FIXED && KH == 4 && BN == 64 && TW == 8 && EPI == EPI_ADD) ? 3
                                                                      : 2;
 }
 
@@ -210,11 +183,6 @@ __global__ void __launch_bounds__(NT, (conv_minw<KH, BN, TW, EPI, SHP::FIXED>())
       *reinterpret_cast<f16x8*>(lds_lo + NPIX * LDP + 8 * tid) = f16x8{};
     }
   }
-#if CH_EXP
-  const unsigned long long ch_t0 = CH_T();
-  unsigned long long ch_sum[5] = {0, 0, 0, 0, 0}, ch_a = 0, ch_b = 0, ch_c = 0;
-  int ch_n = 0;
-#endif
   // layer geometry (compile-time when SHP is a fixed shape: cin, cout are then their padded sizes)
   constexpr bool FX = SHP::FIXED;
   const int A_H = FX ? shp_h<SHP>() : a.h, A_W = FX ? shp_w<SHP>() : a.w;
@@ -371,28 +339,12 @@ __global__ void __launch_bounds__(NT, (conv_minw<KH, BN, TW, EPI, SHP::FIXED>())
     };
     if constexpr (EARLY_B) load_b0();
     else load_pro();
-#if CH_EXP
-    ch_a = CH_T();
-    if (ch == 0) ch_sum[0] = ch_a - ch_t0;
-    else ch_sum[3] += ch_a - ch_c;   // the previous chunk's taps + this chunk's barrier and loads
-#endif
 #pragma unroll
     for (int j = 0; j < MAXT; ++j) {
       const int task = tid + j * NT;
       if (task >= nstg * QPP) continue;
       const int px = task / QPP, q = task % QPP;
       float4 v = pre[j];
-#if CONV_H3_RAWSTAGE
-      // dev timing build: the staging of a producer-split input (the 4 bytes of each element already
-      // hold its fp16 hi / lo) -- no prologue, range check or split
-      {
-        const uint2 u0 = {__builtin_bit_cast(uint32_t, v.x), __builtin_bit_cast(uint32_t, v.y)};
-        const uint2 u1 = {__builtin_bit_cast(uint32_t, v.z), __builtin_bit_cast(uint32_t, v.w)};
-        *reinterpret_cast<uint2*>(lds_hi + px * LDP + q * 4) = u0;
-        *reinterpret_cast<uint2*>(lds_lo + px * LDP + q * 4) = u1;
-        continue;
-      }
-#endif
       if constexpr (PRO != PRO_NONE) {
         if (valid & (1u << j)) {
           const float4 sc = psc, sh = psh;
@@ -419,15 +371,7 @@ __global__ void __launch_bounds__(NT, (conv_minw<KH, BN, TW, EPI, SHP::FIXED>())
       *reinterpret_cast<f16x4*>(lds_hi + px * LDP + q * 4) = hv;
       *reinterpret_cast<f16x4*>(lds_lo + px * LDP + q * 4) = lv;
     }
-#if CH_EXP
-    ch_b = CH_T();
-    ch_sum[1] += ch_b - ch_a;
-#endif
     __syncthreads();
-#if CH_EXP
-    ch_c = CH_T();
-    ch_sum[2] += ch_c - ch_b;
-#endif
 
     // ---- all taps of this chunk ------------------------------------------------------------------
     if constexpr (!EARLY_B) load_b0();
@@ -486,11 +430,6 @@ __global__ void __launch_bounds__(NT, (conv_minw<KH, BN, TW, EPI, SHP::FIXED>())
     }
   }
 
-#if CH_EXP
-  ch_b = CH_T();
-  ch_sum[3] += ch_b - ch_c;
-  ch_n = nchunks;
-#endif
   // ---- epilogue ----------------------------------------------------------------------------------
   if constexpr (CIL) {
     // lane's register quad g holds channels 8 g + 4 (lane >> 5) + 0..3 of tile pixel
@@ -781,23 +720,6 @@ __global__ void __launch_bounds__(NT, (conv_minw<KH, BN, TW, EPI, SHP::FIXED>())
   }
   }   // CIL
   if (rbad && a.range_flag) *a.range_flag = 1;
-#if CH_EXP
-  {
-    const unsigned long long te = CH_T();
-    if (lane == 0 && blockIdx.y == 0 && blockIdx.x < 8192 && a.kh == g_ch_sel[0] && a.kw == g_ch_sel[1] &&
-        a.h == g_ch_sel[2] && a.cin == g_ch_sel[3] && a.cout == g_ch_sel[4]) {
-      unsigned long long* o = g_ch_t + (blockIdx.x * 4 + wave) * 8;
-      o[0] = ch_sum[0];
-      o[1] = ch_sum[1];
-      o[2] = ch_sum[2];
-      o[3] = ch_sum[3];
-      o[4] = te - ch_b;
-      o[5] = te - ch_t0;
-      o[6] = (unsigned long long)ch_n;
-      o[7] = ch_t0;
-    }
-  }
-#endif
 }
 
 template <int KH, int KW, int CK, int BN, int TW, int PRO, int EPI, bool POOL, bool V4 = true,
@@ -868,10 +790,7 @@ hipError_t conv_h3_launch(ConvH3Args a, hipStream_t s) {
     return hipErrorInvalidValue;
   }
   // the fixed OD-NET layers (blocks 4-9 on the 128 x 151 image): compile-time geometry
-#ifndef CONV_H3_FIXED
-#define CONV_H3_FIXED 1
-#endif
-  const bool std_pad = CONV_H3_FIXED && a.pad_h == (a.kh - 1) / 2 && a.pad_w == (a.kw - 1) / 2 &&
+  const bool std_pad = a.pad_h == (a.kh - 1) / 2 && a.pad_w == (a.kw - 1) / 2 &&
                        a.cin == a.cin_pad && a.cout == a.cout_pad;
 #define H3F(KH, KW, TW, E, PL, H, W, CI, CO)                                                     \
   if (std_pad && a.kh == KH && a.kw == KW && ck == 32 && a.tw == TW && a.pro == PRO_BN_ELU &&   \
@@ -939,12 +858,3 @@ void conv_h3_split_weights(const float* w, int kh, int kw, int cin, int cout, in
       }
 }
 
-#if CH_EXP
-extern "C" int mmla_debug_conv_select(int kh, int kw, int h, int cin, int cout) {
-  const int sel[5] = {kh, kw, h, cin, cout};
-  return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_ch_sel), sel, sizeof(sel));
-}
-extern "C" int mmla_debug_conv_times(unsigned long long* host) {
-  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ch_t), sizeof(g_ch_t));
-}
-#endif

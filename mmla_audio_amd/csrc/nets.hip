@@ -195,8 +195,8 @@ __global__ void __launch_bounds__(256) bilstm_kernel(const float* __restrict__ s
 
 // ---- 3xFP16 BiLSTM ----------------------------------------------------------------------------
 // (Round 4: 32 clips per workgroup at two workgroups per CU, or 64 clips at one per CU for batches
-// >= LSTM_MT2_MIN; B by buffer loads one gate ahead; gate reciprocals on v_rcp_f32 -- see LSTM_W4,
-// LSTM_RCP and bilstm_h3_launch.)
+// >= 8192; B by buffer loads one gate ahead; gate reciprocals on v_rcp_f32 -- see lstm_rcp,
+// bilstm_h3_kernel and bilstm_h3_launch.)
 // The same recurrence with the [32 x 384] x [384 x 1024] step product on the f16 MFMA
 // (v_mfma_f32_32x32x16_f16) with 3xFP16 products: A = [h_{t-1} | x_t] split into fp16 hi/lo in LDS,
 // B = the stacked kernels pre-split on the host and packed in MFMA fragment order (a lane's 8
@@ -212,18 +212,11 @@ typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 
 // gate nonlinearities on the hardware exp / rcp (a few ulp from expf / tanhf; far inside the 1e-4
 // probability tolerance)
-// LSTM_RCP 1: v_rcp_f32 (1 ulp) for the reciprocal; 0: __frcp_rn, correctly rounded, which compiles to
+// v_rcp_f32 (1 ulp) for the reciprocal (round 4; __frcp_rn, correctly rounded, compiles to
 // the ~10-instruction IEEE division sequence -- 80 of them per lane and step sit between a step's
 // last MFMA and its barrier
-#ifndef LSTM_RCP
-#define LSTM_RCP 1
-#endif
 MMLA_DEV float lstm_rcp(float x) {
-#if LSTM_RCP
   return __builtin_amdgcn_rcpf(x);
-#else
-  return __frcp_rn(x);
-#endif
 }
 MMLA_DEV float sigm_f(float z) { return lstm_rcp(1.0f + __expf(-z)); }
 MMLA_DEV float tanh_f(float x) { return 1.0f - 2.0f * lstm_rcp(1.0f + __expf(2.0f * x)); }
@@ -248,17 +241,14 @@ MMLA_DEV void split1(float v, _Float16& h, _Float16& l) {   // v * 2^6 = hi + lo
 
 // MT 32-clip row tiles per workgroup (1, or 2 where the batch still fills the chip: half the weight
 // stream per clip); PF: prefetch the next k-step's B fragments (MT 1 only: registers)
-// LSTM_W4 (round 4): two workgroups per CU (4 waves per SIMD, <= 128 VGPRs) instead of one with a
+// (round 4): two workgroups per CU (4 waves per SIMD, <= 128 VGPRs) instead of one with a
 // k-step-ahead B ring at 242 VGPRs.  2 (the product): B fragments one GATE ahead (the next
 // (k-step, gate)'s 2 x 16 B in flight under this gate's 3 MFMAs); 1: loaded right before their MFMAs,
 // the other workgroup's waves hiding the L2 latency.  Bit-identical to 0 (same MFMA order per
 // accumulator).  Measured (A/B, one box): SI LSTM stage 9.36 -> 8.71 ms per 3 steps (2) / 9.31 (1);
 // OD LSTM 23.8 -> 21.7 ms per 3 steps (2); SI 2.63 -> 2.65 M clips/s
-#ifndef LSTM_W4
-#define LSTM_W4 2
-#endif
 template <int D, int MT>
-__global__ void __launch_bounds__(512, (LSTM_W4 && MT == 1) ? 4 : 2) bilstm_h3_kernel(const float* __restrict__ seq, int n, int T,
+__global__ void __launch_bounds__(512, MT == 1 ? 4 : 2) bilstm_h3_kernel(const float* __restrict__ seq, int n, int T,
                                                         const uint16_t* __restrict__ wfh,
                                                         const uint16_t* __restrict__ wfl,
                                                         const uint16_t* __restrict__ wbh,
@@ -273,8 +263,8 @@ __global__ void __launch_bounds__(512, (LSTM_W4 && MT == 1) ? 4 : 2) bilstm_h3_k
   constexpr int LDA = K + 8;             // fp16 per A row (16-B pad)
   constexpr int NTH = 512;
   constexpr int ROWS = 32 * MT;
-  constexpr bool W4 = LSTM_W4 && MT == 1;
-  constexpr bool GA = LSTM_W4 == 2;          // the gate-ahead buffer-load k-loop (any MT)
+  constexpr bool W4 = MT == 1;
+  constexpr bool GA = true;            // the gate-ahead buffer-load k-loop (any MT)
   constexpr bool PF = MT == 1 && !W4;
   __shared__ __attribute__((aligned(16))) _Float16 Ahi[ROWS * LDA];
   __shared__ __attribute__((aligned(16))) _Float16 Alo[ROWS * LDA];
@@ -816,10 +806,7 @@ hipError_t bilstm_h3_launch(const float* seq, int n, int T, int D, const uint16_
   // gives every CU a workgroup per direction: half the per-step weight stream per clip, bit-identical
   // (the same MFMA sequence per clip).  Measured (A/B, one box): SI LSTM 7.56 -> 6.89 ms per 3 steps,
   // OD 18.4 -> 17.0.  Small batches (the batch-1 real-time call) keep 32-clip workgroups, two per CU.
-#ifndef LSTM_MT2_MIN
-#define LSTM_MT2_MIN 8192
-#endif
-  if (n >= LSTM_MT2_MIN) {
+  if (n >= 8192) {
     hipLaunchKernelGGL((bilstm_h3_kernel<128, 2>), dim3(blocks_for(n, 2 * LSTM_ROWS), 2), dim3(512), 0, s,
                        seq, n, T, wfh, wfl, wbh, wbl, bf, bb, out, range_flag, ws_fwd, ws_bwd);
     return hipGetLastError();

@@ -23,23 +23,7 @@
 // ONE accumulator per tile: acc += hi*hi + hi*lo + lo*hi; value = acc * 2^-12.
 #include "resblk.h"
 
-#ifndef RB_W2LDS
-#define RB_W2LDS 0   // block 1: GEMM 2's weights from L2 in fragment order, 3 workgroups per CU (1: in LDS, 2)
-#endif
-#ifndef RB_EXP
-#define RB_EXP 0   // experiment switch for profiling (0 = product)
-#endif
-#if RB_EXP == 4
-// phase timestamps (s_memtime) of the first 8192 workgroups of the pool-block launch
-__device__ unsigned long long g_rb_t[8192 * 4 * 8];
-#define RB_MARK(k)                                                                        \
-  do {                                                                                    \
-    if (POOL && blockIdx.x < 8192 && lane == 0)                                           \
-      g_rb_t[(blockIdx.x * 4 + wave) * 8 + (k)] = __builtin_amdgcn_s_memtime();          \
-  } while (0)
-#else
 #define RB_MARK(k)
-#endif
 
 #include <algorithm>
 #include <cstring>
@@ -53,13 +37,7 @@ typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 constexpr int NT = 256;
 constexpr int TW = 16;
 constexpr int TH = 16;                 // output rows per tile (block 1; blocks 2-3: TH_NP)
-#ifndef RB_MINB_L2
-#define RB_MINB_L2 3
-#endif
-#ifndef RB_TH2
-#define RB_TH2 16
-#endif
-constexpr int TH_NP = RB_TH2;          // output rows per tile of the non-pool blocks 2-3
+constexpr int TH_NP = 16;          // output rows per tile of the non-pool blocks 2-3
 constexpr float ACT_SCALE = 16.0f;     // 2^4: every split activation
 // weights: split at a per-tensor power-of-two scale (resblk_split_weights; the a.u1 / a.u2 / a.us
 // epilogue factors are 2^-4 / that scale)
@@ -85,12 +63,9 @@ __device__ __forceinline__ void split2(f32x2 v, f16x2& h, f16x2& l) {
   l = __builtin_convertvector(v - hf, f16x2);
 }
 
-// RB_BUFB: GEMM 1 / GEMM 2 B fragments by raw buffer loads from a wave-uniform descriptor
+// GEMM 1 / GEMM 2 B fragments by raw buffer loads from a wave-uniform descriptor
 // (voffset = the lane's offset, soffset = the uniform (k-step, tile) offset): no per-load 64-bit
-// address VALU (as conv_h3.hip CONV_H3_BUFB)
-#ifndef RB_BUFB
-#define RB_BUFB 1
-#endif
+// address VALU (as conv_h3.hip h3_frag)
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rb_rsrc(const void* p) {
   const uint64_t u = reinterpret_cast<uint64_t>(p);
   const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)u);
@@ -101,13 +76,8 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rb_rsrc(const void* p) {
 // 16 B of a split weight at half index uoff (wave-uniform) + lofs (this lane's)
 __device__ __forceinline__ f16x8 rb_frag(const uint16_t* base, __amdgpu_buffer_rsrc_t r, int uoff,
                                          int lofs) {
-#if RB_BUFB
   (void)base;
   return __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(r, (uint32_t)lofs * 2u, uoff * 2, 0));
-#else
-  (void)r;
-  return *reinterpret_cast<const f16x8*>(base + uoff + lofs);
-#endif
 }
 
 // the 3 channels of image pixel `pix` (uint8 decoded PNG or float NHWC), as floats
@@ -159,9 +129,9 @@ struct Geo {
   // LDS (51 KB) admits a third workgroup per CU: conv 1432 -> 1386 ms per OD step (A/B).  (With
   // the [co][k] rows and no prefetch the same move had been 7.5 % slower.)  Blocks 2-3 keep them in
   // LDS: without them they still need 60 KB, two workgroups per CU.
-  static constexpr bool W2LDS = CIN == 16 ? RB_W2LDS : TH == 16;
+  static constexpr bool W2LDS = CIN != 16 && TH == 16;
   static constexpr int W2 = W2LDS ? C * LW2 : 0;
-  static constexpr int MINB = W2LDS ? 2 : (TH == 16 ? 3 : RB_MINB_L2);   // resident workgroups per CU
+  static constexpr int MINB = W2LDS ? 2 : 3;   // resident workgroups per CU
   static constexpr int PF = 3;                     // GEMM 1 B fragments in flight (k-steps)
   static constexpr int QPP = CIN / 4;              // float4 per halo pixel
   static constexpr int MAXT = (XNP * QPP + NT - 1) / NT;
@@ -206,7 +176,7 @@ __global__ void __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(R
   // the shortcut operands read both from LDS behind one extra barrier.  Both live past the halo's
   // hi/lo planes, inside bytes that t1 only takes after GEMM 1 (GEMM 1's padded rows may read them:
   // finite fp16 patterns).  Per thread this issues <= 7 loads where the per-task image and per-channel
-  // weight loads were ~50 (RB_EXP timeline: the halo phase was the longest of block 1).
+  // weight loads were ~50 (a phase timeline: the halo phase was the longest of block 1).
   float4* const s_img = reinterpret_cast<float4*>(smem + G::XREG);
   float4* const s_wst = s_img + G::XNP;
   static_assert(!STEM || (G::XREG % 8 == 0 && G::XREG * 2 + (G::XNP + 16) * 16 <= G::SM * 2),
@@ -222,12 +192,8 @@ __global__ void __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(R
       const int py = p / XC, pxx = p - (p / XC) * XC;
       const int ih = h0 - 2 + py, iw = w0 - 1 + pxx;
       if (p < G::XNP && ih >= 0 && ih < a.h && iw >= 0 && iw < a.w) {
-#if RB_EXP == 5   // timing bound: no image loads (garbage outputs)
-        im[k] = make_float4((float)(ih & 255), (float)(iw & 255), (float)(clip & 255), 1.0f);
-#else
         im[k] = image_px(a, ((int64_t)clip * a.h + ih) * a.w + iw);
         im[k].w = 1.0f;
-#endif
       }
     }
     if (tid < 64) {   // [co][k]: k < 3 weights of the r, g, b inputs, k = 3 the bias
@@ -261,13 +227,9 @@ __global__ void __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(R
         const int py = px / XC, pxx = px - (px / XC) * XC;
         const int ih = h0 - 2 + py, iw = w0 - 1 + pxx;
         if (ih >= 0 && ih < a.h && iw >= 0 && iw < a.w) {
-#if RB_EXP == 1
-          pre[j] = make_float4(0.01f * ih, 0.02f * iw, 0.f, 1.f);
-#else
           if constexpr (!STEM) {   // (STEM: from s_img after the barrier below)
             pre[j] = *reinterpret_cast<const float4*>(xc + (ih * a.w + iw) * CIN);
           }
-#endif
           valid |= 1u << j;
         }
       }
@@ -484,10 +446,6 @@ __global__ void __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(R
         const f16x8 al = *reinterpret_cast<const f16x8*>(alb + koff + m * XC * XPS);
 #pragma unroll
         for (int nt = 0; nt < NTW; ++nt) {
-#if RB_EXP == 2
-          acc1[m][nt][0] += (float)ah[0] * (float)ch[nt][0] + (float)al[0] * (float)cl[nt][0];
-          continue;
-#endif
           acc1[m][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, cl[nt], acc1[m][nt], 0, 0, 0);
           acc1[m][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, ch[nt], acc1[m][nt], 0, 0, 0);
           acc1[m][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, ch[nt], acc1[m][nt], 0, 0, 0);
@@ -519,11 +477,6 @@ __global__ void __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(R
         const f32x2 rmask = {rm, rm};
 #pragma unroll
         for (int i = 0; i < 4; i += 2) {
-#if RB_EXP == 3
-          thb[(m * TW + i) * TPS + n] = (_Float16)(acc1[m][nt][i] * rm);
-          tlb[(m * TW + i) * TPS + n] = (_Float16)(acc1[m][nt][i + 1] * rm);
-          continue;
-#endif
           const f32x2 x1 = {acc1[m][nt][i], acc1[m][nt][i + 1]};
           const f32x2 u = elu2(x1 * s2v + c2v);
           // guard only the live t1 rows: the padding rows (>= TR, and outside the image) hold
@@ -590,10 +543,6 @@ __global__ void __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(R
         const f16x8 al = *reinterpret_cast<const f16x8*>(alb + koff + m * TW * TPS);
 #pragma unroll
         for (int nt = 0; nt < NTW; ++nt) {
-#if RB_EXP == 2
-          d1[m][nt][0] += (float)ah[0] * (float)gh[nt][0] + (float)al[0] * (float)gl[nt][0];
-          continue;
-#endif
           d1[m][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, gl[nt], d1[m][nt], 0, 0, 0);
           d1[m][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, gh[nt], d1[m][nt], 0, 0, 0);
           d1[m][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, gh[nt], d1[m][nt], 0, 0, 0);
@@ -696,11 +645,6 @@ hipError_t launch(const ResBlkArgs& a, hipStream_t s) {
 
 }  // namespace
 
-#if RB_EXP == 4
-extern "C" int mmla_debug_resblk_times(unsigned long long* host) {
-  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_rb_t), sizeof(g_rb_t));
-}
-#endif
 
 int resblk_k1pad(int cin) { return (9 * cin + 31) / 32 * 32; }
 

@@ -39,15 +39,12 @@
 #include <cstdlib>
 #include <type_traits>
 
-// SI_F32FB 1: the power spectrum is stored and the filterbank summed in float32 after the float64
+// The power spectrum is stored and the filterbank summed in float32 after the float64
 // FFT and real split (which must stay float64: a tone near Nyquist makes the weak low bins the
 // difference of two huge values); the sums of positive powers are well conditioned, the features
 // move by <= ~3e-6 from the float64 oracle (numpy model on the worst-case tones) against the 1e-4
 // bar.  The float64 sub-segment sums had cost 13 % of the kernel (a build without them: 26.6 ->
 // 23.2 ms per 3 SI steps)
-#ifndef SI_F32FB
-#define SI_F32FB 1
-#endif
 
 namespace {
 
@@ -77,10 +74,10 @@ constexpr int WIN = 888;                        // samples [160 g0 - 8, 160 g0 +
 constexpr int WCH = WIN / 8;                    // 111 16-B chunks
 constexpr int FP = 273;                         // frame region pitch (cd): 16 pass-A rows of 17 + 1
 constexpr int PART = 258;                       // region doubles: P[0..256], then (A, B) sub sums
-// the power spectrum / sub-sum element type (SI_F32FB) and the sub sums' offset in that type
-typedef std::conditional<SI_F32FB != 0, float, double>::type fbt;
-typedef std::conditional<SI_F32FB != 0, float2, double2>::type fbt2;
-constexpr int PSUM = SI_F32FB ? 2 * PART : PART;   // same byte offset either way
+// the power spectrum / sub-sum element type (float32) and the sub sums' offset in that type
+typedef float fbt;
+typedef float2 fbt2;
+constexpr int PSUM = 2 * PART;
 constexpr int LFE = PART + 2 * SI_FE_MAX_SUB;   // then 27 log energies
 static_assert(LFE + 27 <= 2 * FP, "frame region");
 static_assert(NL * 13 * sizeof(float) <= R * FP * sizeof(cd), "epilogue cepstra tile");
@@ -143,27 +140,14 @@ MMLA_DEV void split_power(cd z, cd zr, cd w, double& pk, double& pnk) {
 // ocml's log (~1e-16) is a ~40-instruction routine run 27 times per frame.  The features' tolerance
 // is 1e-4 absolute after the DCT (|coefficient| <= 0.28 over 26 logs) and the lifter (<= 12):
 // the bound stays below 2e-5 even if every term's error had the same sign
-#ifndef SI_EXP
-#define SI_EXP 0   // dev timing bounds (garbage outputs): 1 = no sub-segment sums, 2 = no split either
-#endif
-#ifndef SI_FAST_LOG
-#define SI_FAST_LOG 1
-#endif
 MMLA_DEV double log_pos(double x) {
-#if SI_FAST_LOG
   const double m = __builtin_amdgcn_frexp_mant(x);
   const int e = __builtin_amdgcn_frexp_exp(x);
   const float l2 = __builtin_amdgcn_logf((float)m);
   return ((double)e + (double)l2) * 0.69314718055994530942;
-#else
-  return log(x);
-#endif
 }
 
-#ifndef SI_MINB
-#define SI_MINB 2
-#endif
-__global__ void __launch_bounds__(NT, SI_MINB) si_fe_kernel(SiFeArgs a) {
+__global__ void __launch_bounds__(NT, 2) si_fe_kernel(SiFeArgs a) {
   __shared__ __attribute__((aligned(16))) Smem sm;
   const SiFeTables& tb = *a.tables;
   const int lane = threadIdx.x;
@@ -334,7 +318,7 @@ __global__ void __launch_bounds__(NT, SI_MINB) si_fe_kernel(SiFeArgs a) {
     lds_order();
     // ---- split: P[k] for k = lane, 256 - lane, lane + 64, 192 - lane (+ 128), fbt over Z ----------
 #pragma unroll
-    for (int f = 0; f < (SI_EXP >= 2 ? 0 : R); ++f) {
+    for (int f = 0; f < R; ++f) {
       const cd* Z = sm.z[f];
       fbt* P = reinterpret_cast<fbt*>(sm.z[f]);
       const cd za = Z[lane], zar = Z[(256 - lane) & 255], zb = Z[lane + 64], zbr = Z[192 - lane];
@@ -352,7 +336,7 @@ __global__ void __launch_bounds__(NT, SI_MINB) si_fe_kernel(SiFeArgs a) {
     lds_order();
     // ---- sub-segment sums: A = sum P[k], B = sum (k - bin[s]) P[k] = sum i P + d0 A -------------------
 #pragma unroll
-    for (int s = 0; s < (SI_EXP >= 1 ? 0 : 3); ++s) {
+    for (int s = 0; s < 3; ++s) {
       const int scn = (stask[s] >> 9) & 15;
       if (scn > 0) {
         fbt* Q = reinterpret_cast<fbt*>(sm.z[(stask[s] >> 13) & 3]);

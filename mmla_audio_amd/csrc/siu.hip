@@ -24,9 +24,6 @@
 #include <type_traits>
 
 
-#ifndef SIU_MT4
-#define SIU_MT4 1
-#endif
 
 namespace {
 
@@ -226,10 +223,7 @@ __global__ void __launch_bounds__(64 * NW, 2) siu_kernel(SiuArgs a) {
   // ---- GEMM b: output rows r0 + m, m < R (t1 LDS row of output row m at tap dy: m + dy) -----------
   // EARLY: the residuals of all MT tiles loaded before GEMM b, so their latency hides under it
   // (units without pooling whose registers allow it: MT 2)
-#ifndef SIU_EARLY_RSD
-#define SIU_EARLY_RSD 1
-#endif
-  constexpr bool EARLY = SIU_EARLY_RSD && !POOL && MT <= 2;
+  constexpr bool EARLY = !POOL && MT <= 2;
   float ersd[EARLY ? MT : 1][16];
   if constexpr (EARLY) {
 #pragma unroll
@@ -339,9 +333,9 @@ hipError_t launch(const SiuArgs& a, hipStream_t s) {
 
 }  // namespace
 
-bool siu_supported(int c) { return c == 32 || c == 64 || (SIU_MT4 && c == 128); }
+bool siu_supported(int c) { return c == 32 || c == 64 || c == 128; }
 
-bool siu_final_supported(int c) { return SIU_MT4 && c == 128; }
+bool siu_final_supported(int c) { return c == 128; }
 
 bool sipu_supported(int cin, int c) {
   return (cin == 32 && c == 32) || (cin == 32 && c == 64) || (cin == 64 && c == 128);
@@ -369,14 +363,10 @@ hipError_t siu_launch(const SiuArgs& a, int c, hipStream_t s) {
   // Measured per unit and SI step against the conv_h3 pair: C = 32 1.004 vs 1.033 ms, C = 64 (128-row
   // tiles) 1.061 vs 1.203 ms, C = 128 with 64-row tiles 1.672 vs 1.625 ms (B streamed per 62 output
   // rows); with the MT 4 tiles SI 2.45 -> 2.51 M clips/s (A/B, 2 rounds; the conv stage itself
-  // +0.8 %).  SIU_MT4=0: the 128-row C = 64 tiles, C = 128 on the pair.  Tried: 8-wave workgroups
+  // +0.8 %).  Tried: 8-wave workgroups
   // (one per CU) and 512-row C = 32 tiles (occupancy 1): slower
   if (c == 32) return launch<32, 32, 256, 4>(a, s);
-#if SIU_MT4
   if (c == 64) return launch<64, 64, 256, 4>(a, s);
   if (c == 128) return launch<128, 128, 128, 4>(a, s);
-#else
-  if (c == 64) return launch<64, 64, 128, 4>(a, s);
-#endif
   return hipErrorInvalidValue;
 }
