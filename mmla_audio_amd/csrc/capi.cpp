@@ -337,7 +337,7 @@ int ws_check_guards(mmla_ctx* c) {
 
 enum Slot {
   S_PCM = 0, S_LENS, S_IMG, S_X, S_T1, S_T2, S_T3, S_SEQ, S_HOUT, S_LOGIT, S_FEAT, S_SILENT,
-  S_OUT0, S_OUT1, S_OUT2, S_OUT3, S_IN, S_FESCR,
+  S_OUT0, S_OUT1, S_OUT2, S_OUT3, S_IN,
   S_NR_S, S_NR_BITS, S_NR_FMAX, S_NR_FRAMES, S_NR_ITEMS, S_NR_Y, S_NR_ROWS,
   S_VAD_SPEECH, S_VAD_OUT, S_VAD_LENS, S_RS_TR, S_RS_WIN, S_LSTM
 };
@@ -1306,7 +1306,7 @@ int mmla_create(int device, mmla_ctx** out) {
   }
   OdFeTables ot;
   od_fe_build_tables(&ot);
-  if (!od_fe_tables_ok(ot)) {   // mel tap counts exceed the front-end kernel's unrolled taps
+  if (!od_fe_tables_ok(ot)) {   // the mel schedule exceeds the front-end kernel's LDS rows / fragments
     mmla_destroy(c);
     return MMLA_E_INVALID;
   }
@@ -1636,8 +1636,6 @@ static int od_features_common(mmla_ctx* c, const T* pcm, int64_t n, int64_t stri
   if (!c) return MMLA_E_INVALID;
   if (bad_pcm_args(reinterpret_cast<const int16_t*>(pcm), n, stride, lens, clip_len))
     return fail(c, MMLA_E_INVALID, "bad pcm args");
-  if (std::is_same<T, float>::value && od_fe_needs_scratch())
-    return fail(c, MMLA_E_INVALID, "float PCM needs the MFMA front-end (unset MMLA_OD_FE_V2)");
   HIPCHK(c, hipSetDevice(c->device));
   const bool dev = flags & MMLA_DEVICE_PTR;
   if constexpr (std::is_same<T, float>::value) {
@@ -1673,11 +1671,6 @@ static int od_features_common(mmla_ctx* c, const T* pcm, int64_t n, int64_t stri
     CHK(out_ptr(c, norm, c0 * OD_PIX, cnt * OD_PIX, dev, S_OUT1, &a.norm));
     CHK(out_ptr(c, zcr, c0 * OD_W, cnt * OD_W, dev, S_OUT2, &a.zcr));
     CHK(out_ptr(c, img, c0 * OD_IMG, cnt * OD_IMG, dev, S_OUT3, &a.img));
-    if (od_fe_needs_scratch()) {   // only the A/B v2 kernel keeps a mel-dB scratch in HBM
-      void* ps = nullptr;
-      CHK(ws_get(c, S_FESCR, (size_t)cnt * OD_PIX * sizeof(float), &ps));
-      a.scratch = static_cast<float*>(ps);
-    }
     LAUNCH(c, MMLA_STAGE_OD_FE, od_fe_bytes(cnt, a), od_fe_launch(a, cnt, c->stream));
     CHK(copy_back(c, db, c0 * OD_PIX, a.db, cnt * OD_PIX, dev));
     CHK(copy_back(c, norm, c0 * OD_PIX, a.norm, cnt * OD_PIX, dev));
@@ -1861,11 +1854,6 @@ int mmla_od_pipeline(mmla_ctx* c, const int16_t* pcm, int64_t n, int64_t stride,
       a.clip_len = p.clip_len;
       a.tables = c->od_tables;
       a.img = static_cast<uint8_t*>(pimg);
-      if (od_fe_needs_scratch()) {
-        void* ps = nullptr;
-        CHK(ws_get(c, S_FESCR, (size_t)cnt * OD_PIX * sizeof(float), &ps));
-        a.scratch = static_cast<float*>(ps);
-      }
       LAUNCH(c, MMLA_STAGE_OD_FE, od_fe_bytes(cnt, a), od_fe_launch(a, cnt, c->stream));
       float* dp;
       int32_t* da;

@@ -4,25 +4,16 @@
 #include <stdint.h>
 
 struct OdFeTables {
-  float hann[400];          // periodic Hann (scipy get_window('hann', 400, fftbins=True))
-  float w16[9][2];          // W16^k, k = 0..8
-  float w400[9][25][2];     // W400^(n2*k1)
-  float w25[5][5][2];       // W25^(b*c)
   int mel_start[128];       // first non-zero bin of each Slaney mel band
-  int mel_cnt[128];         // number of non-zero bins (<= 9)
+  int mel_cnt[128];         // number of non-zero bins (<= 10)
   float mel_w[128][10];     // float32 band weights
-  // v2 (200-point complex FFT of the even/odd-packed frame, 20 x 10 Cooley-Tukey)
-  float hann2[200][2];      // (hann[2m], hann[2m + 1]) / 32768
-  float tw[20][10][2];      // W200^(k1 * n2)
-  float w400k[101][2];      // W400^k, k = 0..100 (even/odd split)
-  int mel_taps_lo, mel_taps_hi;   // max non-zeros over bands 0..63 / 64..127
-  // v3 (two-stage matrix DFT on the f16 MFMA, od_fe.hip): the 32x32x16 A fragments of both stages,
+  // two-stage matrix DFT on the f16 MFMA (od_fe.hip): the 32x32x16 A fragments of both stages,
   // fp16 hi / lo bit patterns in fragment order [gemm][k-step][hi, lo][lane][8]
   //   stage 1, gemm n1 = 0..15:  rows c = 2 k2 + ri, k = n2      (window x DFT-25, x 2^8)
   //   stage 2, gemm k2' = 0..12: rows 2 i + ri,    k = 2 n1 + ri (twiddle x DFT-16, x 2^8)
   uint16_t a1[16][2][2][64][8];
   uint16_t a2[13][2][2][64][8];
-  // v3 mel on the f32 MFMA (v_mfma_f32_16x16x4f32): 8 tiles of 16 bands x the two 16-frame halves of
+  // mel on the f32 MFMA (v_mfma_f32_16x16x4f32): 8 tiles of 16 bands x the two 16-frame halves of
   // a 32-frame tile = 16 units, one per wave.  Band tile bt reads P rows mel_bt_bin0[bt] .. + 4 nk - 1
   // (nk = mel_bt_nk[bt], a multiple of 4) against A fragments mel_bt_frag[bt] .. + nk - 1
   int mel_bt_bin0[8], mel_bt_nk[8], mel_bt_frag[8];
@@ -42,13 +33,10 @@ struct OdFeArgs {
   float* norm;              // [n,128,151] nullable
   float* zcr;               // [n,151]     nullable
   uint8_t* img;             // [n,128,151,3] nullable
-  float* scratch;           // [n,151,128] mel-power scratch (frame-major): v2 only
   int* range_flag;          // nullable: set when a float PCM sample is outside the split range
                             // (|y| >= 8188 or not finite: y 2^3 must fit fp16)
 };
 
 void od_fe_build_tables(OdFeTables* t);
-bool od_fe_tables_ok(const OdFeTables& t);   // the mel tap counts fit the kernel's unrolling
-size_t od_fe_smem_bytes();
-bool od_fe_needs_scratch();                  // false for the MFMA kernel (v3, the default)
+bool od_fe_tables_ok(const OdFeTables& t);   // the mel schedule fits the kernel's LDS rows and fragments
 hipError_t od_fe_launch(const OdFeArgs& a, int64_t n_clips, hipStream_t stream);

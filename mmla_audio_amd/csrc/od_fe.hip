@@ -8,21 +8,9 @@
 //   zero_crossing_rate(400, 160)        :100  (edge padding, signbit crossings)
 //   generate_zcr_image + imsave + decode_png   :133-151, record_on_pc.py:156-158
 //
-// v2.  One wave = one clip (64-thread workgroups), frames in rounds of R = 6.  The
-// 400-point real DFT of a frame is ONE 200-point complex FFT of the even/odd-packed frame
-// z[m] = x[2m] + i x[2m+1] followed by the standard split
-//     X[k] = (Z[k] + conj Z[200-k]) / 2 - i W400^k (Z[k] - conj Z[200-k]) / 2,
-// and the 200-point FFT is Cooley-Tukey 20 x 10 with both sub-transforms as prime-factor (Good-
-// Thomas) FFTs (20 = 4 x 5, 10 = 2 x 5: no twiddles inside them):
-//   pass A  (60 lanes = 6 frames x n2 0..9):  DFT-20 over n1 of z[10 n1 + n2], x W200^(n2 k1)
-//   pass B  (2 x 60 lanes = 6 frames x k1):   DFT-10 over n2 -> Z[k1 + 20 k2]
-//   split   (per frame, k = lane, lane + 64): |X[k]|^2 and |X[200 - k]|^2 from Z[k], Z[200 - k]
-//   mel     (lane = bands m, m + 64):         sparse Slaney taps from registers, 10 log10 S
-// Only LDS dependencies inside ONE wave cross lanes in the round loop, and a wave's LDS operations
-// execute in issue order, so the loop has no s_barrier / s_waitcnt vmcnt(0): the next round's
-// window (register prefetch) and the mel-dB scratch stores stay in flight across passes.  The
-// clip's normalisation needs the clip-global max/min, so the dB rows go to a frame-major HBM
-// scratch that the epilogue re-reads (8-band column blocks, transposed through LDS).
+// One persistent 1024-thread workgroup per CU loops over clips; the 400-point DFT runs as two
+// matrix stages on the f16 MFMA in error-compensated 3xFP16 (the v3 kernel below; the earlier
+// VALU-FFT kernels and their measurements are in DESIGN.md section 4).
 //
 // Built WITHOUT packed-FP32 instructions (v_pk_fma/mul/add_f32; Makefile NO_PK_F32): on MI355X a
 // front-end wave using them returned wrong values in one 16-lane quarter of an instruction, a few
@@ -31,7 +19,7 @@
 // (A per-kernel target attribute is not enough: the HIP headers' helpers, e.g. float2's constructor
 // and threadIdx, then stop inlining across the feature mismatch and spill to scratch.)
 //
-// Arithmetic is float32 (the reference runs the FFT in float64 and stores complex64; the measured
+// Accumulation is float32 (the reference runs the FFT in float64 and stores complex64; the measured
 // deviation on the normalised log-mel is ~1e-5, tolerance 1e-4).  The scalar steps
 // that the reference does in float64 (ref dB, image quantisation) are done in float64 here.
 #include "common.h"
@@ -43,28 +31,6 @@
 #include <type_traits>
 #include <utility>
 
-#ifndef FE_EXP
-#define FE_EXP 0   // 1: per-phase s_memtime totals of the first 4096 clips (tools/fe_timeline.py)
-#endif
-#if FE_EXP
-__device__ unsigned long long g_fe_t[4096 * 8];
-#define FE_T_INIT                                              \
-  unsigned long long tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};       \
-  unsigned long long tlast = __builtin_amdgcn_s_memtime();
-#define FE_MARK(k)                                                   \
-  do {                                                               \
-    const unsigned long long tn = __builtin_amdgcn_s_memtime();      \
-    tacc[k] += tn - tlast;                                           \
-    tlast = tn;                                                      \
-  } while (0)
-#define FE_T_STORE                                                   \
-  if (threadIdx.x == 0 && clip < 4096)                                      \
-    for (int i_ = 0; i_ < 8; ++i_) g_fe_t[clip * 8 + i_] = tacc[i_];
-#else
-#define FE_T_INIT
-#define FE_MARK(k)
-#define FE_T_STORE
-#endif
 namespace {
 
 constexpr int N_FFT = 400;
@@ -72,569 +38,6 @@ constexpr int HOP = 160;
 constexpr int CLIP = 24000;
 constexpr int NF = 151;
 constexpr int NMEL = 128;
-constexpr int NT = 64;           // one wave per workgroup (= per clip)
-
-MMLA_DEV void fft4(cf& a0, cf& a1, cf& a2, cf& a3) {
-  cf s02 = cadd(a0, a2), d02 = csub(a0, a2), s13 = cadd(a1, a3), d13 = csub(a1, a3);
-  a0 = cadd(s02, s13);
-  a2 = csub(s02, s13);
-  a1 = cadd(d02, cmul_negi(d13));
-  a3 = csub(d02, cmul_negi(d13));
-}
-
-// complex 8-point DFT in registers (radix-2 DIF + two 4-point DFTs)
-MMLA_DEV void fft8(cf z[8]) {
-  const float r = 0.70710678118654752f;
-  cf a[4], b[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    a[k] = cadd(z[k], z[k + 4]);
-    b[k] = csub(z[k], z[k + 4]);
-  }
-  b[1] = cmul(b[1], cf{r, -r});
-  b[2] = cmul_negi(b[2]);
-  b[3] = cmul(b[3], cf{-r, -r});
-  fft4(a[0], a[1], a[2], a[3]);
-  fft4(b[0], b[1], b[2], b[3]);
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    z[2 * k] = a[k];
-    z[2 * k + 1] = b[k];
-  }
-}
-
-MMLA_DEV void dft5(cf x0, cf x1, cf x2, cf x3, cf x4, cf y[5]) {
-  const float c1 = 0.30901699437494742f, c2 = -0.80901699437494742f;
-  const float s1 = 0.95105651629515357f, s2 = 0.58778525229247313f;
-  cf a1 = cadd(x1, x4), b1 = csub(x1, x4), a2 = cadd(x2, x3), b2 = csub(x2, x3);
-  y[0] = cadd(x0, cadd(a1, a2));
-  cf p1 = {x0.x + c1 * a1.x + c2 * a2.x, x0.y + c1 * a1.y + c2 * a2.y};
-  cf p2 = {x0.x + c2 * a1.x + c1 * a2.x, x0.y + c2 * a1.y + c1 * a2.y};
-  cf q1 = {s1 * b1.x + s2 * b2.x, s1 * b1.y + s2 * b2.y};
-  cf q2 = {s2 * b1.x - s1 * b2.x, s2 * b1.y - s1 * b2.y};
-  y[1] = cadd(p1, cmul_negi(q1));
-  y[4] = csub(p1, cmul_negi(q1));
-  y[2] = cadd(p2, cmul_negi(q2));
-  y[3] = csub(p2, cmul_negi(q2));
-}
-
-// DFT-20 in place, natural order in and out: prime-factor 4 x 5, input n = (5a + 4b) mod 20,
-// output k = (5c + 16d) mod 20 (W20^(nk) = W4^(ac) W5^(bd): no twiddles)
-MMLA_DEV void dft20(cf u[20]) {
-  cf t[5][4];
-#pragma unroll
-  for (int b = 0; b < 5; ++b) {
-    cf a0 = u[(4 * b) % 20], a1 = u[(5 + 4 * b) % 20], a2 = u[(10 + 4 * b) % 20],
-       a3 = u[(15 + 4 * b) % 20];
-    fft4(a0, a1, a2, a3);
-    t[b][0] = a0;
-    t[b][1] = a1;
-    t[b][2] = a2;
-    t[b][3] = a3;
-  }
-#pragma unroll
-  for (int c = 0; c < 4; ++c) {
-    cf y[5];
-    dft5(t[0][c], t[1][c], t[2][c], t[3][c], t[4][c], y);
-#pragma unroll
-    for (int d = 0; d < 5; ++d) u[(5 * c + 16 * d) % 20] = y[d];
-  }
-}
-
-// DFT-10 in place: prime-factor 2 x 5, input n = (5a + 2b) mod 10, output k = (5c + 6d) mod 10
-MMLA_DEV void dft10(cf v[10]) {
-  cf t[5][2];
-#pragma unroll
-  for (int b = 0; b < 5; ++b) {
-    const cf a0 = v[(2 * b) % 10], a1 = v[(5 + 2 * b) % 10];
-    t[b][0] = cadd(a0, a1);
-    t[b][1] = csub(a0, a1);
-  }
-#pragma unroll
-  for (int c = 0; c < 2; ++c) {
-    cf y[5];
-    dft5(t[0][c], t[1][c], t[2][c], t[3][c], t[4][c], y);
-#pragma unroll
-    for (int d = 0; d < 5; ++d) v[(5 * c + 6 * d) % 10] = y[d];
-  }
-}
-
-// power_to_db's per-element term 10 log10(max(amin, S)): v_log_f32 (log2) times 10 log10(2).  Every
-// use in the v2 kernel (elements, clip max, clip min) goes through this one function, so the clip
-// maximum maps to exactly d_max and the normalised maximum to exactly 1, as in the reference.
-MMLA_DEV float db10(float s) { return __log2f(fmaxf(1e-10f, s)) * 3.0102999566398120f; }
-
-// wave-local LDS ordering: a wave's DS operations execute in issue order, so lanes of ONE wave
-// only need the compiler not to move LDS accesses across this point (no s_barrier, no lgkmcnt wait).
-// (FE_LDS_WAIT=1 turns it into an lgkmcnt(0) wait: used in round 2 to rule LDS ordering out as the
-// cause of the co-run corruption that packed-FP32 instructions turned out to cause, common.h.)
-#ifndef FE_LDS_WAIT
-#define FE_LDS_WAIT 0
-#endif
-MMLA_DEV void lds_order() {
-#if FE_LDS_WAIT
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#else
-  asm volatile("" ::: "memory");
-#endif
-}
-
-// ================================================================================================
-namespace v2 {
-
-constexpr int R = 6;                              // frames per round
-constexpr int NR = (NF + R - 1) / R;              // 26 rounds
-constexpr int WIN = (R - 1) * HOP + N_FFT;        // 1200 samples behind one round
-constexpr int T_LO = 2, T_HI = 9;                 // mel taps of bands 0..63 / 64..127 (host-checked)
-
-constexpr int P2W = 212;           // power-row pitch (>= 201 + the widest band's taps: zero pad)
-// 12.5 KB: three clip-waves per SIMD (12 per CU).  The power spectra of frame pair q live in the
-// pair's own FFT rows: p2(q)[k].c = P[2q + c][k] over the first 1696 B of st[2q], st[2q + 1] (the
-// split reads both frames' Z before it writes the pair's row)
-//
-// A clip is NW waves (one workgroup): wave w runs rounds w, w + NW, ... in its own LDS buffers,
-// the clip max / min are combined through LDS at one barrier, and the epilogue's 16 band blocks
-// are split over the waves.  Finer work units than one wave per clip shorten the tail of a
-// launch whose clip count is not a multiple of the resident clip-waves (256 CUs x 12 waves): NW 4
-// for small launches (config 2's 4096 clips: 12.8 -> 13.1 M clips/s), NW 2 for large ones (at
-// 65 536 clips NW 4 is 2 % slower than NW 2, which equals NW 1 there) -- A/B, one box.
-struct WaveBuf {
-  int16_t win[WIN];                // reflect-padded window of the round, base = 160 f0 - 200
-  cf st[R][200];                   // per frame: pass A out [k1][n2] -> Z[k] -> power rows
-};
-template <int NW>
-struct Smem {
-  WaveBuf w[NW];
-  int zc[NF + 1];                  // ZCR counts of the clip
-  uint8_t rb[NF + 1];              // image R byte per column
-  float red[2][NW];                // per-wave max / min of the mel power
-};
-[[maybe_unused]] constexpr int64_t NW4_MAX_CLIPS = 8192;   // (A/B builds) launches up to this size use four waves per clip
-static_assert(sizeof(int16_t) * WIN % 16 == 0, "st must stay 16-B aligned");
-static_assert(sizeof(WaveBuf) % 16 == 0, "wave buffers stay 16-B aligned");
-static_assert(P2W * sizeof(float2) <= 2 * 200 * sizeof(cf), "a pair's power row fits its FFT rows");
-MMLA_DEV float2* p2row(WaveBuf& ws, int q) { return reinterpret_cast<float2*>(ws.st[2 * q]); }
-
-// |X[k]|^2 and |X[200 - k]|^2 of the 400-point real DFT from Z[k], Z[200 - k] of the packed FFT
-MMLA_DEV void split_power(cf z, cf zr, cf w, float& pk, float& pnk) {
-  const cf h = {0.5f * (z.x + zr.x), 0.5f * (z.y - zr.y)};   // (Z[k] + conj Z[-k]) / 2 = E[k]
-  const cf b = {0.5f * (z.x - zr.x), 0.5f * (z.y + zr.y)};   // (Z[k] - conj Z[-k]) / 2 = i O[k]
-  const cf wb = cmul(w, b);
-  const cf c = {-wb.y, wb.x};                                 // i W^k B / 2
-  const cf x0 = csub(h, c);                                   // X[k]
-  const cf x1 = cadd(h, c);                                   // conj X[200 - k]
-  pk = fmaf(x0.x, x0.x, x0.y * x0.y);
-  pnk = fmaf(x1.x, x1.x, x1.y * x1.y);
-}
-
-// DB / NM / IMG: which of the dB, normalised and image outputs are written (compile-time, so the
-// epilogue's store counts are static and its waits for the scratch re-reads stay counted)
-template <int NW, bool DB, bool NM, bool IMG>
-#ifndef FE_MINB
-#define FE_MINB 3   // waves (= workgroups) per SIMD the register budget is sized for (12.5 KB LDS: 12 per CU)
-#endif
-__global__ void __launch_bounds__(NT * NW, FE_MINB) od_fe_kernel(OdFeArgs a) {
-  __shared__ __attribute__((aligned(16))) Smem<NW> sm;
-  const OdFeTables& tb = *a.tables;
-  const int lane = threadIdx.x & (NT - 1);
-  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / NT);
-  WaveBuf& ws = sm.w[wid];
-  const int64_t clip = blockIdx.x;
-
-  int len = a.lens ? a.lens[clip] : a.clip_len;
-  len = len < 0 ? 0 : (len > CLIP ? CLIP : len);
-  const int16_t* src = a.pcm + clip * a.clip_stride;
-  float* scr = a.scratch + clip * (NMEL * NF);
-  // edge padding of the ZCR: samples before / after the clip repeat its first / last sample
-  const int sg_first = (len > 0 ? src[0] : (int16_t)0) < 0;
-  const int sg_last = (CLIP - 1 < len ? src[CLIP - 1] : (int16_t)0) < 0;
-
-  // the window of round r + 1 is loaded into registers (16-B chunks) while round r computes; rounds
-  // whose window leaves [0, len) take the scalar reflect / zero-fill path instead
-  constexpr int WCH = WIN / 8;                      // 150 chunks
-  constexpr int WPL = (WCH + NT - 1) / NT;          // 3 per lane
-  const bool vec_ok = ((reinterpret_cast<uintptr_t>(src) & 15) == 0);
-  auto fast = [&](int r_) {
-    const int b_ = HOP * R * r_ - N_FFT / 2;
-    return vec_ok && b_ >= 0 && b_ + WIN <= len;
-  };
-  // three named registers (an indexed array behind a lambda was demoted to scratch memory, whose
-  // loads wait on vmcnt(0) -- i.e. on every outstanding store)
-  static_assert(WPL == 3, "window chunks per lane");
-  const bool l2 = lane < WCH - 2 * NT;              // lanes holding a third chunk
-  uint4 nx0 = {0, 0, 0, 0}, nx1 = {0, 0, 0, 0}, nx2 = {0, 0, 0, 0};
-#define FE_PREFETCH(r_)                                                                   \
-  do {                                                                                    \
-    const uint4* s4_ = reinterpret_cast<const uint4*>(src + HOP * R * (r_) - N_FFT / 2);  \
-    nx0 = s4_[lane];                                                                      \
-    nx1 = s4_[lane + NT];                                                                 \
-    nx2 = s4_[l2 ? lane + 2 * NT : WCH - 1];   /* unconditional: a static load count */   \
-  } while (0)
-  if (fast(wid)) FE_PREFETCH(wid);
-
-  // this lane's two mel bands: first bin and the band's taps (zero past its non-zeros)
-  const int mlo = tb.mel_start[lane], mhi = tb.mel_start[lane + 64];
-  float wlo[T_LO], whi[T_HI];
-#pragma unroll
-  for (int j = 0; j < T_LO; ++j) wlo[j] = tb.mel_w[lane][j];
-#pragma unroll
-  for (int j = 0; j < T_HI; ++j) whi[j] = tb.mel_w[lane + 64][j];
-  // keep the taps in registers: without this the compiler re-loads them from global memory every
-  // round, and those loads' vmcnt waits also drain the round's outstanding scratch stores
-#pragma unroll
-  for (int j = 0; j < T_LO; ++j) asm volatile("" : "+v"(wlo[j]));
-#pragma unroll
-  for (int j = 0; j < T_HI; ++j) asm volatile("" : "+v"(whi[j]));
-
-  FE_T_INIT
-  // split twiddles W400^k of the lane's two bins, and the pass-A window taps of its n2: per-lane
-  // constants kept in registers (LDS reads every frame / round otherwise)
-  const cf wka = {tb.w400k[lane][0], tb.w400k[lane][1]};
-  const cf wkb = lane + 64 <= 100 ? cf{tb.w400k[lane + 64][0], tb.w400k[lane + 64][1]} : cf{0.f, 0.f};
-  // pass A: window taps of the lane's n2; pass B: twiddles W200^(n2 k1) of the lane's k1 (applied
-  // when pass B reads the row: 9 per lane instead of pass A's 19 -- the registers that let three
-  // waves share a SIMD)
-  cf hw[20], tk[10];
-  {
-    const int n2 = lane < R * 10 ? lane % 10 : 0;
-#pragma unroll
-    for (int n1 = 0; n1 < 20; ++n1) hw[n1] = cf{tb.hann2[10 * n1 + n2][0], tb.hann2[10 * n1 + n2][1]};
-    const int k1 = lane < 60 ? lane % 20 : 0;
-#pragma unroll
-    for (int j = 1; j < 10; ++j) tk[j] = cf{tb.tw[k1][j][0], tb.tw[k1][j][1]};
-  }
-  static_assert(R % 2 == 0, "frame pairs");
-
-  float smax = 0.0f, smin = INFINITY;
-  for (int r = wid; r < NR; r += NW) {
-    const int f0 = r * R;
-    const int base = HOP * f0 - N_FFT / 2;
-    lds_order();   // the previous round's mel reads of st are issued
-    // ---- window: reflect padding for the STFT (centre=True, pad_mode='reflect') ------------------
-    if (fast(r)) {
-      uint4* w4 = reinterpret_cast<uint4*>(ws.win);
-      w4[lane] = nx0;
-      w4[lane + NT] = nx1;
-      if (l2) w4[lane + 2 * NT] = nx2;
-    } else {
-      // all of the lane's scalar loads are issued before the first is consumed (one wait)
-      constexpr int SPL = (WIN + NT - 1) / NT;       // 19
-      int16_t v[SPL];
-#pragma unroll
-      for (int j = 0; j < SPL; ++j) {
-        const int w = lane + NT * j;
-        int i = base + w;
-        i = i < 0 ? -i : i;
-        i = i >= CLIP ? 2 * (CLIP - 1) - i : i;
-        v[j] = (w < WIN && i < len) ? src[i] : (int16_t)0;
-      }
-#pragma unroll
-      for (int j = 0; j < SPL; ++j)
-        if (lane + NT * j < WIN) ws.win[lane + NT * j] = v[j];
-    }
-    if (r + NW < NR && fast(r + NW)) FE_PREFETCH(r + NW);
-    lds_order();
-    FE_MARK(0);
-    // ---- zero crossings (edge padding, signbit semantics): lane l < 60 owns window positions
-    //      w = 20 l .. 20 l + 19 and counts the transitions (w - 1, w) among them from a sign-bit
-    //      mask (five 8-B LDS reads); frame f covers lanes 8 f .. 8 f + 19 minus position 160 f (its
-    //      first transition is outside the frame) --------------------------------------------------
-    {
-      constexpr int ZCH = 20, ZL = WIN / ZCH;      // 60 lanes
-      static_assert(WIN % ZCH == 0 && HOP % ZCH == 0 && N_FFT % ZCH == 0, "ZCR chunking");
-      int cl = 0, first = 0;
-      if (lane < ZL) {
-        const int w0 = ZCH * lane;
-        const uint2* wp = reinterpret_cast<const uint2*>(ws.win + w0);   // 40 B per lane
-        uint32_t m = 0;                              // bit j: signbit of window sample w0 + j
-#pragma unroll
-        for (int k = 0; k < ZCH / 4; ++k) {
-          const uint2 d = wp[k];
-          // high bytes of the four samples, then their top bits gathered into a nibble
-          const uint32_t hb = __builtin_amdgcn_perm(d.y, d.x, 0x07050301u);
-          const uint32_t nib = (((hb >> 7) & 0x01010101u) * 0x01020408u) >> 24;
-          m |= (nib & 0xfu) << (4 * k);
-        }
-        // bit j of e: signbit of the sample at w0 - 1 + j (j = 0..20)
-        uint32_t e = (m << 1) | (w0 > 0 ? (uint32_t)(ws.win[w0 - 1] < 0) : 0u);
-        const int i0 = base + w0 - 1;                // clip index of bit 0
-        if (i0 < 0 || i0 + ZCH >= CLIP) {            // edge padding outside the clip
-          const int nlo = min(max(-i0, 0), ZCH + 1);
-          const int jhi = min(max(CLIP - i0, 0), ZCH + 1);
-          const uint32_t lo = (1u << nlo) - 1u, hi = ((1u << (ZCH + 1)) - 1u) & ~((1u << jhi) - 1u);
-          e = (e & ~lo & ~hi) | (sg_first ? lo : 0u) | (sg_last ? hi : 0u);
-        }
-        uint32_t t = (e ^ (e >> 1)) & ((1u << ZCH) - 1u);   // bit j: transition into w0 + j
-        if (w0 == 0) t &= ~1u;                       // no sample before the window
-        cl = __builtin_popcount(t);
-        first = (int)(t & 1u);
-      }
-      int* scan = reinterpret_cast<int*>(ws.st);   // st is free until pass A writes it
-      scan[lane] = cl;
-      scan[NT + lane] = first;
-      lds_order();
-      int c = 0, fz = 0;
-      if (lane < R) {
-        const int4* s4 = reinterpret_cast<const int4*>(scan + 8 * lane);
-#pragma unroll
-        for (int l = 0; l < 5; ++l) {
-          const int4 v = s4[l];
-          c += v.x + v.y + v.z + v.w;
-        }
-        fz = scan[NT + 8 * lane];
-      }
-      lds_order();   // scan reads are issued before pass A overwrites st
-      if (lane < R && f0 + lane < NF) sm.zc[f0 + lane] = c - fz;
-    }
-    FE_MARK(1);
-    // ---- pass A: DFT-20 over n1 of z[10 n1 + n2] (z[m] = hann-windowed (x[2m], x[2m+1]))
-    //      -> st[f][k1][n2] (the twiddle W200^(n2 k1) is applied by pass B) ---------------------------
-    if (lane < R * 10) {
-      const int f = lane / 10, n2 = lane - 10 * f;
-      const uint32_t* wp = reinterpret_cast<const uint32_t*>(ws.win) + 80 * f + n2;
-      cf u[20];
-#pragma unroll
-      for (int n1 = 0; n1 < 20; ++n1) {
-        const uint32_t w = wp[10 * n1];
-        const cf h = hw[n1];
-        u[n1] = {(float)(int)(int16_t)(w & 0xffffu) * h.x, (float)((int)w >> 16) * h.y};
-      }
-      dft20(u);
-      cf* dst = &ws.st[f][n2];
-#pragma unroll
-      for (int k1 = 0; k1 < 20; ++k1) dst[10 * k1] = u[k1];
-    }
-    lds_order();
-    FE_MARK(2);
-    // ---- pass B: twiddle, then DFT-10 over n2 of row st[f][k1][*] -> Z[k1 + 20 k2], in place per frame
-    //      (frames 0-2, then 3-5: a round never reads a frame the other one writes; all of a
-    //      round's reads are issued before its writes) -------------------------------------------------
-#pragma unroll
-    for (int rr = 0; rr < 2; ++rr) {
-      if (lane < 60) {
-        const int f = 3 * rr + lane / 20, k1 = lane % 20;
-        const float4* row = reinterpret_cast<const float4*>(&ws.st[f][10 * k1]);
-        cf v[10];
-#pragma unroll
-        for (int j = 0; j < 5; ++j) {
-          const float4 q = row[j];
-          v[2 * j] = {q.x, q.y};
-          v[2 * j + 1] = {q.z, q.w};
-        }
-        lds_order();
-#pragma unroll
-        for (int j = 1; j < 10; ++j) v[j] = cmul(v[j], tk[j]);
-        dft10(v);
-#pragma unroll
-        for (int k2 = 0; k2 < 10; ++k2) ws.st[f][k1 + 20 * k2] = v[k2];
-      }
-      lds_order();
-    }
-    FE_MARK(3);
-    // ---- split: power spectra P[f][0..200] of frame pair q into the pair's interleaved row, which
-    //      overlays the pair's Z rows: both frames' Z are read before the first write -------------------
-#pragma unroll
-    for (int q = 0; q < R / 2; ++q) {
-      const int ka = lane, kb = lane + 64;
-      const bool hb = kb <= 100;
-      cf za[2], zar[2], zb[2] = {{0.f, 0.f}, {0.f, 0.f}}, zbr[2] = {{0.f, 0.f}, {0.f, 0.f}};
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        const cf* Z = ws.st[2 * q + c];
-        za[c] = Z[ka];
-        zar[c] = Z[ka == 0 ? 0 : 200 - ka];
-        if (hb) {
-          zb[c] = Z[kb];
-          zbr[c] = Z[200 - kb];
-        }
-      }
-      lds_order();
-      float* P = reinterpret_cast<float*>(p2row(ws, q));   // P[2q + c][k] at P[2 k + c]
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        float p0, p1;
-        split_power(za[c], zar[c], wka, p0, p1);
-        P[2 * ka + c] = p0;
-        P[2 * (200 - ka) + c] = p1;
-        if (hb) {
-          split_power(zb[c], zbr[c], wkb, p0, p1);
-          P[2 * kb + c] = p0;
-          P[2 * (200 - kb) + c] = p1;
-        }
-      }
-      if (lane < 2 * (P2W - 201)) P[2 * 201 + lane] = 0.0f;   // the row pad read by the last taps
-    }
-    lds_order();
-    FE_MARK(4);
-    // ---- mel: S[m][f] = sum_j w[m][j] P[f][start_m + j] -> 10 log10 S to the frame-major scratch ---
-    // two frames per packed FMA (the pair's interleaved power row); taps past a band's non-zeros
-    // are exact zeros times finite LDS words (the row pad is zeroed): same sum.  Every round issues
-    // the same 12 stores (frames past the clip, last round only, repeat the round's first frame):
-    // the compiler can then count them in the next round's window wait
-    float s0 = 0.0f, s1 = 0.0f;
-#pragma unroll
-    for (int q = 0; q < R / 2; ++q) {
-      const float2* P = p2row(ws, q);
-      float2 a0 = {0.0f, 0.0f}, a1 = {0.0f, 0.0f};
-#pragma unroll
-      for (int j = 0; j < T_LO; ++j) {
-        const float2 v = P[mlo + j];
-        a0 = float2{fmaf(wlo[j], v.x, a0.x), fmaf(wlo[j], v.y, a0.y)};
-      }
-#pragma unroll
-      for (int j = 0; j < T_HI; ++j) {
-        const float2 v = P[mhi + j];
-        a1 = float2{fmaf(whi[j], v.x, a1.x), fmaf(whi[j], v.y, a1.y)};
-      }
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        const int f = 2 * q + c;
-        float b0 = c ? a0.y : a0.x, b1 = c ? a1.y : a1.x;
-        if (f == 0) {
-          s0 = b0;
-          s1 = b1;
-        } else if (f0 + f >= NF) {
-          b0 = s0;
-          b1 = s1;
-        }
-        float* row = scr + min(f0 + f, NF - 1) * NMEL;
-        row[lane] = db10(b0);
-        row[lane + 64] = db10(b1);
-        smax = fmaxf(smax, fmaxf(b0, b1));
-        smin = fminf(smin, fminf(b0, b1));
-      }
-    }
-    FE_MARK(5);
-  }
-  // ---- clip max / min of the mel power (one wave: shuffles only) ----------------------------------
-  smax = wave_max(smax);
-  smin = wave_min(smin);
-  wave_stores_done();   // this wave's scratch stores have completed (common.h)
-  if (lane == 0) {
-    sm.red[0][wid] = smax;
-    sm.red[1][wid] = smin;
-  }
-  __syncthreads();      // every wave's scratch rows, ZCR counts and max / min are in place
-  smax = sm.red[0][0];
-  smin = sm.red[1][0];
-#pragma unroll
-  for (int w = 1; w < NW; ++w) {
-    smax = fmaxf(smax, sm.red[0][w]);
-    smin = fminf(smin, sm.red[1][w]);
-  }
-
-  // power_to_db(ref=np.max, amin=1e-10, top_db=80) with numpy-1.21 dtypes, then normalize_matrix.
-  // log10 is monotone, so max/min of the dB matrix are the dB of max/min S.  Each numpy op rounds
-  // separately: no FMA contraction from here on.
-  {
-#pragma clang fp contract(off)
-  const float ref_db = (float)(10.0 * log10(fmax(1e-10, (double)smax)));
-  const float d_max = db10(smax) - ref_db;
-  const float thr = d_max - 80.0f;
-  const float d_min = fmaxf(db10(smin) - ref_db, thr);
-  const float diff = d_max - d_min;
-
-  float* db_out = a.db + clip * (NMEL * NF);      // dereferenced only when DB
-  float* nm_out = a.norm + clip * (NMEL * NF);    // only when NM
-  if (a.zcr) {
-    for (int f = threadIdx.x; f < NF; f += NT * NW) a.zcr[clip * NF + f] = (float)sm.zc[f] * (1.0f / 400.0f);
-  }
-  // LDS of the round loop is free: [8][151] band-major tiles of normalised / dB values, i.e. the
-  // output layout itself (a block of 8 bands is 1208 contiguous floats of [128][151])
-  constexpr int MB = 8;                                    // bands per column block
-  constexpr int BLK = MB * NF;                             // 1208 floats = 302 float4
-  float* nvt = reinterpret_cast<float*>(ws.win);           // [MB][NF] over the wave's win + st
-  float* dbt = nvt + BLK;                                  // [MB][NF]
-  static_assert(sizeof(WaveBuf) >= 2 * BLK * sizeof(float), "LDS tiles");
-  static_assert(BLK % 4 == 0, "16-B tile rows");
-  if (IMG) {
-    for (int w = threadIdx.x; w < NF; w += NT * NW) sm.rb[w] = (uint8_t)(int)(((double)sm.zc[w] / 400.0) * 255.0);
-    __syncthreads();
-  }
-  const float inv_diff = 1.0f / diff;
-  // the block's scratch reads are issued one block ahead (registers); with static store counts the
-  // compiler's wait for them is vmcnt(N), not a drain of the previous block's output stores
-  constexpr int RPL = (BLK / 4 + NT - 1) / NT;             // float4 per lane per block (5)
-  float4 cur[RPL], nx[RPL];
-#define FE_FETCH(mb_)                                                                          \
-  do {                                                                                         \
-    _Pragma("unroll") for (int q_ = 0; q_ < RPL; ++q_) {                                       \
-      const int i_ = min(lane + NT * q_, BLK / 4 - 1);   /* clamped, not branched: static   */  \
-      const int t_ = i_ / (MB / 4), qd_ = i_ - t_ * (MB / 4); /* load count per block       */  \
-      nx[q_] = *reinterpret_cast<const float4*>(scr + t_ * NMEL + MB * (mb_) + 4 * qd_);       \
-    }                                                                                          \
-  } while (0)
-  static_assert((NMEL / MB) % NW == 0, "band blocks per wave");
-  FE_FETCH(wid);
-  for (int mb = wid; mb < NMEL / MB; mb += NW) {
-#pragma unroll
-    for (int q = 0; q < RPL; ++q) cur[q] = nx[q];
-    if (mb + NW < NMEL / MB) FE_FETCH(mb + NW);
-    lds_order();   // the previous block's tile reads are issued
-#pragma unroll
-    for (int q = 0; q < RPL; ++q) {                           // frame t, quad of bands
-      const int i = lane + NT * q;
-      if (i >= BLK / 4) break;
-      const int t = i / (MB / 4), qd = i - t * (MB / 4);
-      const float pv[4] = {cur[q].x, cur[q].y, cur[q].z, cur[q].w};
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        float d = pv[j] - ref_db;   // pv = 10 log10(max(amin, S)) from the mel pass
-        d = fmaxf(d, thr);
-        if (DB) dbt[(4 * qd + j) * NF + t] = d;
-        // normalize_matrix's (x - min) / (max - min) as a multiply by the reciprocal: <= 2 ulp from
-        // the division (image quantisation flips <= 1 LSB on ~1e-5 of pixels); 0 * inf = NaN
-        // keeps the digital-silence NaN
-        nvt[(4 * qd + j) * NF + t] = (d - d_min) * inv_diff;
-      }
-    }
-    lds_order();
-    if (DB || NM) {                                           // rows m = 8 mb .. 8 mb + 7
-#pragma unroll
-      for (int q = 0; q < RPL; ++q) {
-        // lanes past the block rewrite its last float4 with the same bytes: no branch around the
-        // stores, so every block issues the same number of them
-        const int e4 = min(lane + NT * q, BLK / 4 - 1);
-        if (DB) reinterpret_cast<float4*>(db_out + BLK * mb)[e4] = reinterpret_cast<const float4*>(dbt)[e4];
-        if (NM) reinterpret_cast<float4*>(nm_out + BLK * mb)[e4] = reinterpret_cast<const float4*>(nvt)[e4];
-      }
-    }
-    if (IMG) {
-      // image rows h = 127 - m: the block is 8 whole rows of 453 B, word aligned
-      // R = trunc(255 * zcr[w]) (float64), G = B = trunc(255 * (1 - norm)) (float64: numpy-1.21
-      // '1 - np.float32' promotes); NaN -> 0
-      const int h_lo = NMEL - MB * (mb + 1);
-      uint32_t* out = reinterpret_cast<uint32_t*>(a.img + clip * (NMEL * NF * 3) + h_lo * NF * 3);
-      // one lane = 4 consecutive pixels of the block (row-major) = 12 bytes = 3 words
-#pragma unroll
-      for (int q = 0; q < RPL; ++q) {
-        const int qd = lane + NT * q;
-        if (qd >= BLK / 4) break;
-        uint32_t by[12];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int p = 4 * qd + j;
-          const int hr = p / NF, w = p - hr * NF;
-          const double v = (1.0 - (double)nvt[(MB - 1 - hr) * NF + w]) * 255.0;
-          const uint32_t gb = (v >= 0.0) ? ((uint32_t)(int)v & 255u) : 0u;   // NaN fails v >= 0
-          by[3 * j] = sm.rb[w];
-          by[3 * j + 1] = gb;
-          by[3 * j + 2] = gb;
-        }
-#pragma unroll
-        for (int k = 0; k < 3; ++k)
-          out[3 * qd + k] = by[4 * k] | (by[4 * k + 1] << 8) | (by[4 * k + 2] << 16) | (by[4 * k + 3] << 24);
-      }
-    }
-  }
-#undef FE_FETCH
-  }
-  FE_MARK(6);
-  FE_T_STORE
-}
-
-}  // namespace v2
-
 // ================================================================================================
 // v3: the 400-point windowed real DFT as two matrix stages on the f16 MFMA, whole clips per
 // persistent workgroup, the clip's mel-dB values in registers until its max / min are known (no
@@ -650,7 +53,7 @@ __global__ void __launch_bounds__(NT * NW, FE_MINB) od_fe_kernel(OdFeArgs a) {
 //       starts at n1 = 0 or 8 of one q row ... so n2 runs contiguous: 16-B fragment reads)
 //   stage 2 (wave = k2', 13 GEMMs): D2[row][f] = sum_k A2[k2'][row][k] Z[k2'][k][f], k = 2 n1 + ri,
 //       rows = (re, im) of bins 25 i + k2' and 25 (i - 8) + 25 - k2' (i < 8; conj Y folded into A2)
-//   power |X|^2 -> P[bin][f] (LDS) -> sparse Slaney mel on the VALU (lane = band m and m + 64, as v2)
+//   power |X|^2 -> P[bin][f] (LDS) -> Slaney mel on the f32 MFMA (16-band x 4-bin A fragments)
 //
 // Arithmetic: error-compensated 3xFP16 with f32 accumulation (x' = x 2^-12 splits int16 exactly into
 // fp16 hi + lo; A1 x 2^9, A2 x 2^7 so their lo halves stay normal (Z = 2 Y: |Z| < 51200, lo normal
@@ -664,17 +67,7 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef uint16_t us2 __attribute__((ext_vector_type(2)));
 
-#ifndef FE3_NWV
-#define FE3_NWV 16
-#endif
-#ifndef FE3_PRIO
-#define FE3_PRIO 0
-#endif
-#ifndef FE3_SKIP
-#define FE3_SKIP 0   // dev timing builds only: 1 staging, 2 stage 1, 4 stage 2, 8 mel, 16 norm stores skipped;
-                     // 32 / 64 / 128: the mel / stage-1 / stage-2 MFMAs replaced by one VALU op each
-#endif
-constexpr int NWV = FE3_NWV;                  // waves per workgroup (one workgroup per CU)
+constexpr int NWV = 16;                       // waves per workgroup (one workgroup per CU)
 constexpr int NTH = 64 * NWV;
 constexpr int TF = 32;                        // frames per tile = the MFMA's 32 columns
 constexpr int NTILE = (NF + TF - 1) / TF;     // 5 (frames 151..159 are computed and dropped)
@@ -691,10 +84,6 @@ constexpr int PTRASH = PROWS;                 // + one row that stage 2's unused
 constexpr int G1 = 16 / NWV;                  // stage-1 GEMMs (n1) per wave
 constexpr int G2 = (13 + NWV - 1) / NWV;      // stage-2 GEMMs (k2') per wave (the last round partial)
 constexpr int MFRAG = 64;                     // mel A fragments (16 bands x 4 bins each)
-#ifndef FE3_MEL_A_W0
-#define FE3_MEL_A_W0 16   // measured: 12 (the youngest wave of each SIMD in A) 0.2964 ms, 8: 0.2944, 14: 0.3054, 16: 0.2941
-#endif
-constexpr int MEL_A_W0 = FE3_MEL_A_W0;         // waves >= this run the mel in interval A (16: none)
 constexpr int ROT4 = 9;                       // tile 4: chunk c is staged by thread c + ROT4
 static_assert(NCH + ROT4 <= NTH, "one staged chunk per thread");
 static_assert(G1 == 1, "stage 1: one GEMM per wave (16 waves)");
@@ -795,28 +184,6 @@ MMLA_DEV float wave_red(float v) {
   return op(op(r0, r1), op(r2, r3));
 }
 
-#if !FE_EXP
-#define FE3_T_INIT
-#define FE3_MARK(k)
-#define FE3_T_STORE(clip_)
-#else
-#define FE3_T_INIT                                                   \
-  unsigned long long tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};             \
-  unsigned long long tlast = __builtin_amdgcn_s_memtime();
-#define FE3_MARK(k)                                                  \
-  do {                                                               \
-    const unsigned long long tn = __builtin_amdgcn_s_memtime();      \
-    tacc[k] += tn - tlast;                                           \
-    tlast = tn;                                                      \
-  } while (0)
-#define FE3_T_STORE(clip_)                                           \
-  do {                                                               \
-    if (lane == 0 && (clip_) < 4096 / NWV)                           \
-      for (int i_ = 0; i_ < 8; ++i_) g_fe_t[((clip_) * NWV + wid) * 8 + i_] = tacc[i_]; \
-    for (int i_ = 0; i_ < 8; ++i_) tacc[i_] = 0;                     \
-  } while (0)
-#endif
-
 template <int T>
 using tile_c = std::integral_constant<int, T>;
 template <class F, int... I>
@@ -871,14 +238,9 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
     asm volatile("" : "+v"(v));
     return v;
   };
-  // the staging thread order starts at wave SW0 (chunk c is staged by thread c + 64 (16 - SW0), mod
-  // 1024): which waves carry interval B's staging beside the mel and stage 2
-#ifndef FE3_SW0
-#define FE3_SW0 0   // 13 (waves 13-15 first) was best with the mel in interval A; with it in B, 0:
-                    //   0.2899 vs 0.2936 ms (8: 0.2951), A/B 3 rounds
-#endif
-  constexpr int SW0 = FE3_SW0;
-  auto stid = [&]() { return (otid() + (NWV - SW0) * 64) & (NTH - 1); };
+  // the staging thread order: chunk c is staged by thread c (starting at other waves, e.g. 13-15
+  // first, measured 0.2936 vs 0.2899 ms with the mel in interval B)
+  auto stid = [&]() { return otid(); };
   static_assert(NWV == 16, "staging order assumes 16 waves");
 
   // clip facts the staging needs, wave-uniform
@@ -932,7 +294,6 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
   //      x' = x 2^-12 into fp16 hi + lo, transposed store T[p & 15][p >> 4] = (hi, lo) ---------------
   auto stage = [&](int64_t clip, auto T_) {
     constexpr int t = decltype(T_)::value;
-    if constexpr (FE3_SKIP & 1) return;
     const ClipIn ci = clip_in(clip);
     const int c = stid() - (t == NTILE - 1 ? ROT4 : 0);
     const int i0 = HOP * TF * t - N_FFT / 2 + 8 * c;
@@ -974,10 +335,10 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
       // 465..489) take their samples from the chunks they mirror, lanes of the same wave:
       //   tile 0: p' = 400 - p  -> chunk 49 - c elements 8 - j (j >= 1), chunk 50 - c element 0
       //   tile 4: p' = 7438 - p -> chunk 929 - c elements 6 - j (j <= 6), chunk 928 - c element 7
-      // (staging wave = (first ? 0 : (465 + ROT4) / 64) in the staging order, i.e. that + SW0 mod 16)
+      // (staging wave = first ? 0 : (465 + ROT4) / 64)
       if constexpr (t == 0 || t == NTILE - 1) {
         constexpr bool first = t == 0;
-        if (wid == ((first ? 0 : (465 + ROT4) / 64) + SW0) % NWV) {
+        if (wid == (first ? 0 : (465 + ROT4) / 64)) {
           const int pa = first ? 49 - c : 929 - c, pb = first ? 50 - c : 928 - c;
           const int la = (pa + (first ? 0 : ROT4)) & 63, lb = (pb + (first ? 0 : ROT4)) & 63;
           uint32_t ma[4], mb;
@@ -1051,7 +412,6 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
 
   // ---- stage 1 (wave = n1 G1 wid .. + G1 - 1): D1 = A1[n1] (32 x 32) . B1 (32 n2 x 32 frames) ------
   auto stage1 = [&](int r, int hh) {
-    if constexpr (FE3_SKIP & 2) return;
     f32x16 acc[G1];
 #pragma unroll
     for (int g = 0; g < G1; ++g) {
@@ -1075,10 +435,6 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
           bl[i] = __builtin_amdgcn_perm(w[2 * i + 1], w[2 * i], 0x07060302u);
         }
         const f16x8 BH = __builtin_bit_cast(f16x8, bh), BL = __builtin_bit_cast(f16x8, bl);
-        if constexpr (FE3_SKIP & 64) {   // dev: stage 1 without its MFMAs (operands still consumed)
-          acc[g][s] += (float)(BH[0] + BL[1]) + (float)a1h[g][s][0];
-          continue;
-        }
         acc[g] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1l[g][s], BH, acc[g], 0, 0, 0);
         acc[g] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1h[g][s], BL, acc[g], 0, 0, 0);
         acc[g] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1h[g][s], BH, acc[g], 0, 0, 0);
@@ -1116,7 +472,7 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
 #pragma unroll
     for (int j = 0; j < G2; ++j) {
       const int k2 = wid + NWV * j;
-      if (k2 >= 13 || (FE3_SKIP & 4)) continue;
+      if (k2 >= 13) continue;
       const uint2* zh = reinterpret_cast<const uint2*>(sm.z_hi + (k2 * TF + r) * ZP + 8 * hh);
       const uint2* zl = reinterpret_cast<const uint2*>(sm.z_lo + (k2 * TF + r) * ZP + 8 * hh);
       f32x16 acc = {};
@@ -1126,10 +482,6 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
         const uint2 h0 = zh[4 * s], h1 = zh[4 * s + 1], l0 = zl[4 * s], l1 = zl[4 * s + 1];
         const f16x8 BH = __builtin_bit_cast(f16x8, uint4{h0.x, h0.y, h1.x, h1.y});
         const f16x8 BL = __builtin_bit_cast(f16x8, uint4{l0.x, l0.y, l1.x, l1.y});
-        if constexpr (FE3_SKIP & 128) {   // dev: stage 2 without its MFMAs (operands still consumed)
-          acc[s] += (float)(BH[0] + BL[1]) + (float)a2h[j][s][0];
-          continue;
-        }
         acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a2l[j][s], BH, acc, 0, 0, 0);
         acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a2h[j][s], BL, acc, 0, 0, 0);
         acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a2h[j][s], BH, acc, 0, 0, 0);
@@ -1207,7 +559,7 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
     constexpr int NK_MAX = 20;
 #pragma unroll
     for (int j0 = 0; j0 < NK_MAX; j0 += 4) {
-      if ((FE3_SKIP & 8) || j0 >= nk) break;
+      if (j0 >= nk) break;
       float av[4], bv[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -1216,8 +568,7 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
       }
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        if constexpr (FE3_SKIP & 32) acc[j] = fmaf(av[j], bv[j], acc[j]);   // dev: the MFMA's cost alone
-        else acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j], bv[j], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j], bv[j], acc, 0, 0, 0);
       }
     }
     const bool live = TF * t + TF <= NF || TF * t + 16 * m_fh + (l & 15) < NF;
@@ -1233,7 +584,7 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
 
   // ---- a clip's end: max / min of its mel power over the waves, power_to_db(ref=np.max, amin=1e-10,
   //      top_db=80) with numpy-1.21 dtypes, normalize_matrix (max / min of the dB matrix are the dB
-  //      of max / min S, as v2), stores straight from the registers -----------------------------------
+  //      of max / min S), stores straight from the registers -----------------------------------
   auto epilogue = [&](int64_t clip, int par) {
 #pragma clang fp contract(off)
     float mx = sm.red[0][0], mn = sm.red[1][0];
@@ -1281,12 +632,12 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const float d = fmaxf(fmaf(dbv[t][i], DB_PER_LOG2, nref), thr);
-        // (d - min) / (max - min) as a multiply by the reciprocal (<= 2 ulp; as v2); 0 * inf =
+        // (d - min) / (max - min) as a multiply by the reciprocal (<= 2 ulp); 0 * inf =
         // NaN keeps the digital-silence NaN.  The (i, t) part of the offset is wave-uniform: it
         // rides in soffset (a scalar add), the lane's part is the one VGPR vf
         const float nv = (d - d_min) * inv_diff;
         const int so = sf + (i * NF + TF * t) * 4;
-        if (NM && !(FE3_SKIP & 16)) __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, nv), rn, vf, so, 0);
+        if (NM) __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, nv), rn, vf, so, 0);
         if (DB) __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, d), rd, vf, so, 0);
         if (IMG) {
           const double v = (1.0 - (double)nv) * 255.0;
@@ -1301,14 +652,6 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
   };
 
   const int64_t my_clips = (int64_t)blockIdx.x < n_clips ? (n_clips - 1 - blockIdx.x) / gridDim.x + 1 : 0;
-#if FE3_PRIO
-  // static issue priority by dispatch age (the SIMD's four waves are wid, wid + 4, wid + 8, wid + 12):
-  // the youngest, the arbitration losers that end every barrier interval, go first
-  if (wid >= 12) __builtin_amdgcn_s_setprio(3);
-  else if (wid >= 8) __builtin_amdgcn_s_setprio(2);
-  else if (wid >= 4) __builtin_amdgcn_s_setprio(1);
-#endif
-  FE3_T_INIT
   if (my_clips > 0) {
     prefetch(blockIdx.x, tile_c<0>{});
     stage(blockIdx.x, tile_c<0>{});
@@ -1335,8 +678,8 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
       const int pw = (int)((ci * NTILE + t) & 1);
       float* const p_w = sm.p[pw];
       const float* const p_r = sm.p[pw ^ 1];
-      // the mel of the previous step reads P[(s - 1) & 1], stable through intervals A and B of step s:
-      // waves >= MEL_A_W0 (the youngest of each SIMD, last to finish the heavier interval B) run it in A
+      // the mel of the previous step reads P[(s - 1) & 1], stable through intervals A and B of step s
+      // (it runs in B on every wave: the youngest waves of each SIMD in A measured 0.2964 vs 0.2941 ms)
       auto mel_prev = [&]() {
         if constexpr (t > 0) {
           mel(tile_c<t - 1>{}, p_r);
@@ -1344,7 +687,6 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
           mel(tile_c<NTILE - 1>{}, p_r);
         }
       };
-      const bool mel_a = wid >= MEL_A_W0;
       // ---- interval A ----
       if (cur) {
         crossings(T_);
@@ -1352,17 +694,12 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
       }
       if (t == 1 && ci > 0) {   // the previous clip: its last mel and max / min finished in step 0
         epilogue(clip - gridDim.x, par ^ 1);
-        FE3_MARK(4);
-        FE3_T_STORE(clip - gridDim.x);
       }
-      if (mel_a) mel_prev();   // (after the epilogue: tile 0's mel overwrites the dB registers it read)
-      FE3_MARK(0);
       __syncthreads();
-      FE3_MARK(1);
       if (!cur && t == 1) return;
       // ---- interval B ----  (the mel of tile t - 1 first: its MFMAs then start on every wave at the
       // barrier instead of queueing behind stage 2's on waves 0-12 -- 0.2975 -> 0.2903 ms, A/B)
-      if (!mel_a) mel_prev();
+      mel_prev();   // (after the epilogue: tile 0's mel overwrites the dB registers it read)
       if (t == 0 && ci > 0) {
         const float mx = wave_red<true>(smax), mn = wave_red<false>(smin);
         if (lane == 0) {
@@ -1386,9 +723,7 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
           prefetch(ci + 1 < my_clips ? clip + gridDim.x : n_clips, tile_c<t + 2 - NTILE>{});
         }
       }
-      FE3_MARK(2);
       __syncthreads();
-      FE3_MARK(3);
     }, std::make_integer_sequence<int, NTILE>{});
   }
   if (fbad && a.range_flag) *a.range_flag = 1;
@@ -1396,22 +731,12 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
 
 }  // namespace v3
 
-
 }  // namespace
 
-#if FE_EXP
-extern "C" int mmla_debug_fe_times(unsigned long long* host) {
-  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_fe_t), sizeof(g_fe_t));
-}
-#endif
-
-size_t od_fe_smem_bytes() { return sizeof(v2::Smem<4>); }
-
 bool od_fe_tables_ok(const OdFeTables& t) {
-  if (t.mel_taps_lo > v2::T_LO || t.mel_taps_hi > v2::T_HI) return false;
-  for (int m = 0; m < 128; ++m) {  // the last tap of every band stays inside the zero-padded row
-    if (t.mel_start[m] + (m < 64 ? v2::T_LO : v2::T_HI) > v2::P2W) return false;
-    const int bt = m / 16;   // v3: the band's support lies inside its tile's bins, read rows stay in P
+  for (int m = 0; m < 128; ++m) {
+    if (t.mel_cnt[m] > 10) return false;   // the weights kept per band (mel_w)
+    const int bt = m / 16;   // the band's support lies inside its tile's bins, read rows stay in P
     if (t.mel_cnt[m] > 0 && (t.mel_start[m] < t.mel_bt_bin0[bt] ||
                              t.mel_start[m] + t.mel_cnt[m] > t.mel_bt_bin0[bt] + 4 * t.mel_bt_nk[bt]))
       return false;
@@ -1426,48 +751,6 @@ bool od_fe_tables_ok(const OdFeTables& t) {
   if (frags > v3::MFRAG) return false;
   return true;
 }
-
-#ifndef OD_FE_V2_AB
-#define OD_FE_V2_AB 0
-#endif
-#if OD_FE_V2_AB
-template <int NW>
-static void launch_nw(const OdFeArgs& a, int64_t n, hipStream_t s) {
-  const dim3 g((unsigned)n), b(NT * NW);
-  const int k = (a.db ? 4 : 0) | (a.norm ? 2 : 0) | (a.img ? 1 : 0);
-  switch (k) {
-    case 0: hipLaunchKernelGGL((v2::od_fe_kernel<NW, false, false, false>), g, b, 0, s, a); break;
-    case 1: hipLaunchKernelGGL((v2::od_fe_kernel<NW, false, false, true>), g, b, 0, s, a); break;
-    case 2: hipLaunchKernelGGL((v2::od_fe_kernel<NW, false, true, false>), g, b, 0, s, a); break;
-    case 3: hipLaunchKernelGGL((v2::od_fe_kernel<NW, false, true, true>), g, b, 0, s, a); break;
-    case 4: hipLaunchKernelGGL((v2::od_fe_kernel<NW, true, false, false>), g, b, 0, s, a); break;
-    case 5: hipLaunchKernelGGL((v2::od_fe_kernel<NW, true, false, true>), g, b, 0, s, a); break;
-    case 6: hipLaunchKernelGGL((v2::od_fe_kernel<NW, true, true, false>), g, b, 0, s, a); break;
-    default: hipLaunchKernelGGL((v2::od_fe_kernel<NW, true, true, true>), g, b, 0, s, a); break;
-  }
-}
-
-static void launch_v2(const OdFeArgs& a, int64_t n, hipStream_t s) {
-  if (n <= v2::NW4_MAX_CLIPS) launch_nw<4>(a, n, s);
-  else launch_nw<2>(a, n, s);
-}
-#endif
-
-// v2 (VALU FFT + HBM scratch) is not in the product build: a dev A/B build
-// (make variant VSRC=od_fe VDEF="-DOD_FE_V2_AB=1 ...") selects it with MMLA_OD_FE_V2=1
-static bool use_v2() {
-#if OD_FE_V2_AB
-  static const bool v = [] {
-    const char* e = getenv("MMLA_OD_FE_V2");
-    return e && e[0] == '1';
-  }();
-  return v;
-#else
-  return false;
-#endif
-}
-
-bool od_fe_needs_scratch() { return use_v2(); }
 
 static void launch_v3(const OdFeArgs& a, int64_t n, hipStream_t s) {
   // persistent: one 1024-thread workgroup per CU (LDS ~119 KB), each looping over clips
@@ -1494,46 +777,12 @@ static void launch_v3(const OdFeArgs& a, int64_t n, hipStream_t s) {
 
 hipError_t od_fe_launch(const OdFeArgs& a, int64_t n_clips, hipStream_t stream) {
   if (n_clips <= 0) return hipSuccess;
-#if OD_FE_V2_AB
-  if (use_v2()) {
-    if (!a.scratch || a.pcm_f32) return hipErrorInvalidValue;
-    launch_v2(a, n_clips, stream);
-    return hipGetLastError();
-  }
-#endif
   launch_v3(a, n_clips, stream);
   return hipGetLastError();
 }
 
 void od_fe_build_tables(OdFeTables* t) {
   const double PI = 3.14159265358979323846;
-  for (int n = 0; n < N_FFT; ++n) t->hann[n] = (float)(0.5 - 0.5 * cos(2.0 * PI * n / N_FFT));
-  for (int m = 0; m < 200; ++m) {   // exact power-of-two scaling of the float32 window
-    t->hann2[m][0] = t->hann[2 * m] * (1.0f / 32768.0f);
-    t->hann2[m][1] = t->hann[2 * m + 1] * (1.0f / 32768.0f);
-  }
-  for (int k1 = 0; k1 < 20; ++k1)
-    for (int n2 = 0; n2 < 10; ++n2) {
-      t->tw[k1][n2][0] = (float)cos(2.0 * PI * k1 * n2 / 200.0);
-      t->tw[k1][n2][1] = (float)-sin(2.0 * PI * k1 * n2 / 200.0);
-    }
-  for (int k = 0; k <= 100; ++k) {
-    t->w400k[k][0] = (float)cos(2.0 * PI * k / 400.0);
-    t->w400k[k][1] = (float)-sin(2.0 * PI * k / 400.0);
-  }
-  for (int k = 0; k < 9; ++k) {
-    t->w16[k][0] = (float)cos(2.0 * PI * k / 16.0);
-    t->w16[k][1] = (float)-sin(2.0 * PI * k / 16.0);
-    for (int n2 = 0; n2 < 25; ++n2) {
-      t->w400[k][n2][0] = (float)cos(2.0 * PI * n2 * k / 400.0);
-      t->w400[k][n2][1] = (float)-sin(2.0 * PI * n2 * k / 400.0);
-    }
-  }
-  for (int b = 0; b < 5; ++b)
-    for (int c = 0; c < 5; ++c) {
-      t->w25[b][c][0] = (float)cos(2.0 * PI * b * c / 25.0);
-      t->w25[b][c][1] = (float)-sin(2.0 * PI * b * c / 25.0);
-    }
   // librosa.filters.mel(16000, 400, n_mels=128, fmin=0, fmax=8000, htk=False, norm='slaney'):
   // float64 triangles stored float32, then float32 * float64 enorm -> float32.
   auto hz_to_mel = [](double f) {
@@ -1554,7 +803,6 @@ void od_fe_build_tables(OdFeTables* t) {
     const double m = (i == NMEL + 1) ? mmax : mmin + i * step;
     mel_f[i] = mel_to_hz(m);
   }
-  t->mel_taps_lo = t->mel_taps_hi = 0;
   t->zero16 = 0;
   for (int m = 0; m < NMEL; ++m) {
     int st = -1, cnt = 0;
@@ -1578,8 +826,6 @@ void od_fe_build_tables(OdFeTables* t) {
     t->mel_start[m] = st < 0 ? 0 : st;
     t->mel_cnt[m] = cnt;
     for (int j = 0; j < 10; ++j) t->mel_w[m][j] = j < cnt ? w[j] : 0.0f;
-    int& taps = m < 64 ? t->mel_taps_lo : t->mel_taps_hi;
-    taps = cnt > taps ? cnt : taps;
   }
 
   // v3 mel schedule: band tile bt = bands 16 bt .. 16 bt + 15 reads the bins of their union, in
@@ -1610,17 +856,13 @@ void od_fe_build_tables(OdFeTables* t) {
   // units (bt, frame half) onto waves: longest first onto the SIMD with the least MFMA work so far,
   // four units per SIMD (a SIMD runs waves s, s + 4, s + 8, s + 12).  The mel shares interval B with
   // stage 2, whose 13 GEMMs (6 MFMAs of the mel K-step's 32 cycles each) sit on waves 0-12: SIMD 0
-  // starts with 4 of them, the others with 3 (FE3_MEL_S2LOAD 0: mel work alone)
-#ifndef FE3_MEL_S2LOAD
-#define FE3_MEL_S2LOAD 1
-#endif
+  // starts with 4 of them, the others with 3 (1 0: mel work alone)
   {
     int order[16];
     for (int u = 0; u < 16; ++u) order[u] = u;
     std::stable_sort(order, order + 16, [&](int x, int y) { return t->mel_bt_nk[x >> 1] > t->mel_bt_nk[y >> 1]; });
     int load[4] = {0, 0, 0, 0}, fill[4] = {0, 0, 0, 0};
-    if (FE3_MEL_S2LOAD)
-      for (int w = 0; w < 13; ++w) load[w % 4] += 6;
+    for (int w = 0; w < 13; ++w) load[w % 4] += 6;
     for (int k = 0; k < 16; ++k) {
       int best = -1;
       for (int s_ = 0; s_ < 4; ++s_)
