@@ -78,7 +78,8 @@ constexpr int NCH = TQS * 16 / 8;             // 670 chunks of 8 samples staged 
 constexpr int ZP = 36;                        // Z row pitch (halves): 18 dwords -- stage 1's dword stores
                                               // of 32 frame rows 2-way (free; 40 was 4-way, ~6 k LDS
                                               // conflict cycles per clip), stage 2's 8-B reads conflict-free
-constexpr int PP = 34;                        // P row pitch (floats)
+constexpr int PP = 32;                        // P row pitch (floats): frame f of bin b at column f ^ (16 (b & 1)),
+                                              //   so the mel's 2 x 16-lane reads of bins b, b + 1 hit 32 banks
 constexpr int PROWS = 212;                    // bins 0..200 + zero rows read by the last mel taps
 constexpr int PTRASH = PROWS;                 // + one row that stage 2's unused lanes write
 constexpr int G1 = 16 / NWV;                  // stage-1 GEMMs (n1) per wave
@@ -489,7 +490,10 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
       // pair i = c0 + 2 hh (c0 = (pi & 1) + 4 (pi >> 1)): bin 25 i + k2 (i < 8: c0 < 8), else
       // 25 (i - 8) + 25 - k2; GEMM 0 has bins 25 i for i <= 8 only (the other lanes write the
       // trash row).  Branch-free: the row offset is an immediate plus the wave-uniform k2
-      float* prow = P + 50 * PP * hh + r;
+      // frame r of an even bin at column r, of an odd bin at r ^ 16 (PP above); a bin's parity is
+      // that of c0 + k2 (rows 25 c0 + 50 hh + k2) or c0 + 1 + k2 (rows 25 (c0 - 8) + 50 hh + 25 - k2)
+      float* const prow0 = P + 50 * PP * hh + r;
+      float* const prow1 = P + 50 * PP * hh + (r ^ 16);
       // one scalar branch per GEMM (not per pair): the k2 = 0 GEMM's row pattern apart, so the other
       // twelve waves store each power with one immediate-offset write from two base registers
       if (k2 == 0) {
@@ -499,17 +503,19 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
           const int c0 = (pi & 1) + 4 * (pi >> 1);
           if (c0 > 8) continue;
           const float pw = fmaf(acc[2 * pi], acc[2 * pi], acc[2 * pi + 1] * acc[2 * pi + 1]);
-          *(c0 + 2 * hh <= 8 ? prow + 25 * c0 * PP : trash) = pw;
+          *(c0 + 2 * hh <= 8 ? (c0 & 1 ? prow1 : prow0) + 25 * c0 * PP : trash) = pw;
         }
       } else {
-        float* const pa = prow + k2 * PP;            // bins 25 c0 + k2       (c0 < 8)
-        float* const pb = prow + (25 - k2) * PP;     // bins 25 (c0 - 8) + 25 - k2
+        float* const qa = (k2 & 1) ? prow1 : prow0;  // rows of parity (c0 + k2) & 1 for even c0
+        float* const qb = (k2 & 1) ? prow0 : prow1;
+        float* const pa0 = qa + k2 * PP, * const pa1 = qb + k2 * PP;                // bins 25 c0 + k2 (c0 < 8)
+        float* const pb0 = qb + (25 - k2) * PP, * const pb1 = qa + (25 - k2) * PP;  // bins 25 (c0 - 8) + 25 - k2
 #pragma unroll
         for (int pi = 0; pi < 8; ++pi) {
           const int c0 = (pi & 1) + 4 * (pi >> 1);
           const float pw = fmaf(acc[2 * pi], acc[2 * pi], acc[2 * pi + 1] * acc[2 * pi + 1]);
-          if (c0 < 8) pa[25 * c0 * PP] = pw;
-          else pb[25 * (c0 - 8) * PP] = pw;
+          if (c0 < 8) (c0 & 1 ? pa1 : pa0)[25 * c0 * PP] = pw;
+          else (c0 & 1 ? pb1 : pb0)[25 * (c0 - 8) * PP] = pw;
         }
       }
     }
@@ -551,7 +557,8 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
     constexpr int t = decltype(T_)::value;
     int l = lane;
     asm volatile("" : "+v"(l));
-    const float* pb = P + (m_bin0 + (l >> 4)) * PP + 16 * m_fh + (l & 15);
+    const int mb = m_bin0 + (l >> 4);   // + 4 k per K-step: the same parity
+    const float* pb = P + mb * PP + ((16 * m_fh + (l & 15)) ^ (16 * (mb & 1)));
     const float* ab = sm.ma + m_frag * 64 + l;
     f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
     int nk = m_nk;
