@@ -5,6 +5,16 @@
 
 #define MMLA_DEV __device__ __forceinline__
 
+// XCD-aware workgroup order (MI355X_MICROARCH.md, workgroup dispatch): blocks b and b + 8 share an
+// XCD's L2, so the logical id handed to a kernel puts consecutive ids on one XCD -- neighbouring
+// tiles of one clip, whose input halos overlap, then meet in the same L2.  Bijective for any count.
+MMLA_DEV uint32_t xcd_block_id() {
+  const uint32_t nwg = gridDim.x, orig = blockIdx.x;
+  const uint32_t xcd = orig % 8u, q = nwg / 8u, r = nwg % 8u;
+  return (xcd < r ? xcd * (q + 1u) : r * (q + 1u) + (xcd - r) * q) + orig / 8u;
+}
+
+
 struct cf {  // complex float held in two VGPRs
   float x, y;
 };

@@ -103,8 +103,9 @@ __global__ void __launch_bounds__(64 * NW, MINW) odu_kernel(OduArgs a) {
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave - (wave / WN) * WN;
-  const int64_t clip = blockIdx.x / TLW;
-  const int w0 = (int)(blockIdx.x - clip * TLW) * TW;
+  const uint32_t bid = xcd_block_id();
+  const int64_t clip = bid / TLW;
+  const int w0 = (int)(bid - clip * TLW) * TW;
   const float* __restrict__ xc = a.x + clip * ((int64_t)H * W * CIN);
   const int koff = (lane >> 5) * 8;
   const int hsel = 4 * (lane >> 5);

@@ -21,6 +21,7 @@
 // K runs over (tap, channel) with the channel fastest, so CIN = 16 packs two taps per k-step.
 // 3xFP16 as in conv_h3.hip: activations x 2^4 and weights x 2^8 split into hi + lo (lo unscaled),
 // ONE accumulator per tile: acc += hi*hi + hi*lo + lo*hi; value = acc * 2^-12.
+#include "common.h"
 #include "resblk.h"
 
 #define RB_MARK(k)
@@ -157,8 +158,9 @@ __global__ void __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(R
   const int wn = wave % WN, wm = wave / WN;
   const int col = lane & 15, grp = lane >> 4;
   const int tiles = a.tiles_h * a.tiles_w;
-  const int clip = blockIdx.x / tiles;
-  const int tile = blockIdx.x - clip * tiles;
+  const int bid = (int)xcd_block_id();
+  const int clip = bid / tiles;
+  const int tile = bid - clip * tiles;
   const int th_i = tile / a.tiles_w;
   constexpr int TH = G::TH;
   const int h0 = th_i * TH, w0 = (tile - th_i * a.tiles_w) * TW;
