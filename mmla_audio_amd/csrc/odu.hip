@@ -91,9 +91,13 @@ __global__ void __launch_bounds__(64 * NW, MINW) odu_kernel(OduArgs a) {
   constexpr int TLW = (W + TW - 1) / TW;
   constexpr int XP = TW + 2, XH = H + 2, NXP = XH * XP;   // x halo: rows -1 .. H, columns -1 .. TW
   constexpr int LDX = CK + 8;                             // fp16 per staged x pixel (16-B pad)
+  // fp16 per halo row: padded so that GEMM a's 16-lane ds_read_b128 groups (8 rows x 2 columns at
+  // TW 2, 4 x 4 at TW 4) hit 64 distinct banks -- 352 / 576 B instead of 320 / 480 (2-way conflicts;
+  // the LDS plane of every instantiation keeps its size: t1 or the LDS limit per CU bound it)
+  constexpr int XRP = TW == 2 ? 176 : TW == 4 ? 288 : XP * LDX;
   constexpr int T1R = H + 3, NT1 = T1R * TW;              // t1 rows -1 .. H + 1 (three zero rows)
   constexpr int LDT = C + 8;                              // fp16 per t1 pixel
-  constexpr int PLANE = NXP * LDX > NT1 * LDT ? NXP * LDX : NT1 * LDT;
+  constexpr int PLANE = XH * XRP > NT1 * LDT ? XH * XRP : NT1 * LDT;
   constexpr int NCHX = CIN / CK, NCH = C / CK;
   constexpr int QPP = CK / 4;                             // float4 per pixel and chunk
   constexpr int MAXT = (NXP * QPP + NT - 1) / NT;
@@ -170,8 +174,9 @@ __global__ void __launch_bounds__(64 * NW, MINW) odu_kernel(OduArgs a) {
         f16x4 hv, lv;
         split4(v, hv, lv);
         const int px = task / QPP;
-        *reinterpret_cast<f16x4*>(lhi + px * LDX + 4 * q) = hv;
-        *reinterpret_cast<f16x4*>(llo + px * LDX + 4 * q) = lv;
+        const int xo = (px / XP) * XRP + (px % XP) * LDX + 4 * q;
+        *reinterpret_cast<f16x4*>(lhi + xo) = hv;
+        *reinterpret_cast<f16x4*>(llo + xo) = lv;
       }
       __syncthreads();
 #pragma unroll
@@ -191,7 +196,7 @@ __global__ void __launch_bounds__(64 * NW, MINW) odu_kernel(OduArgs a) {
 #pragma unroll
           for (int mt = 0; mt < MT; ++mt) {
             const int m = mpix[mt];
-            const int off = ((m / TW + dy) * XP + m % TW + dx) * LDX + 16 * s + koff;
+            const int off = (m / TW + dy) * XRP + (m % TW + dx) * LDX + 16 * s + koff;
             const f16x8 ah = *reinterpret_cast<const f16x8*>(lhi + off);
             const f16x8 al = *reinterpret_cast<const f16x8*>(llo + off);
             acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(bl[s], ah, acc[mt], 0, 0, 0);
