@@ -175,11 +175,24 @@ __global__ void __launch_bounds__(NT, 2) si_fe_kernel(SiFeArgs a) {
     }
     if (a.silent && lane == 0) a.silent[blk] = 0;
   }
-  const int64_t T = len <= 400 ? 1 : 1 + (len - 400 + 159) / 160;   // framesig numframes
-  const int64_t lbase = frame0 - HALO;                               // global frame of local 0
-  const int64_t g_lo = lbase < 0 ? 0 : lbase;
-  const int64_t g_hi = lbase + NL < T ? lbase + NL : T;
-  const int nr = g_hi > g_lo ? (int)((g_hi - g_lo + R - 1) / R) : 0;
+  const int64_t T64 = len <= 400 ? 1 : 1 + (len - 400 + 159) / 160;   // framesig numframes
+  // Window-relative 32-bit coordinates (64-bit index arithmetic was ~90 VALU per round): frames count
+  // from gs, the window's first existing frame; samples from so = 160 gs - soff (soff = 16 past the
+  // first window keeps the round's 8 leading samples at non-negative offsets and xw 16-B aligned as x).
+  // T and the readable length are capped past everything the window reads (frames < NL + 4 apart,
+  // samples < 160 NL + 888), so every comparison below has the outcome it has in global coordinates.
+  const int64_t lb64 = frame0 - HALO;                                // global frame of local 0
+  const int64_t gs = lb64 < 0 ? 0 : lb64;
+  const int soff = gs > 0 ? 16 : 0;
+  const int16_t* const xw = x + (160 * gs - soff);
+  const int64_t lrem = len - (160 * gs - soff);
+  const int lenw = (int)(lrem < 160 * NL + 1024 ? lrem : 160 * NL + 1024);
+  const int64_t trem = T64 - gs;
+  const int T = (int)(trem < NL + 16 ? trem : NL + 16);
+  const int lbase = (int)(lb64 - gs);                                // -4 .. 0
+  constexpr int g_lo = 0;
+  const int g_hi = lbase + NL < T ? lbase + NL : T;
+  const int nr = g_hi > g_lo ? (g_hi - g_lo + R - 1) / R : 0;
 
   // ---- per-lane constants (registers for the whole loop) -----------------------------------------
   const int fq = lane >> 4, q = lane & 15;      // pass A (f, n2) / pass B (f, k1)
@@ -219,24 +232,24 @@ __global__ void __launch_bounds__(NT, 2) si_fe_kernel(SiFeArgs a) {
   const double dsg = (dcc & 1) ? -1.0 : 1.0;
 
   // ---- the round's window: register prefetch one round ahead when it lies inside [0, len) --------
-  const bool vec_ok = (reinterpret_cast<uintptr_t>(x) & 15) == 0;
-  auto fast = [&](int64_t g0_) {
-    const int64_t b_ = 160 * g0_ - 8;
-    return vec_ok && b_ >= 0 && b_ + WIN <= len;
+  const bool vec_ok = (reinterpret_cast<uintptr_t>(xw) & 15) == 0;
+  auto fast = [&](int g0_) {
+    const int b_ = 160 * g0_ + soff - 8;
+    return vec_ok && b_ >= 0 && b_ + WIN <= lenw;
   };
   const bool l1 = lane < WCH - NT;
   uint4 nx0 = {0, 0, 0, 0}, nx1 = {0, 0, 0, 0};
 #define SI_PREFETCH(g0_)                                                         \
   do {                                                                           \
-    const uint4* s4_ = reinterpret_cast<const uint4*>(x + 160 * (g0_) - 8);      \
+    const uint4* s4_ = reinterpret_cast<const uint4*>(xw + 160 * (g0_) + soff - 8); \
     nx0 = s4_[lane];                                                             \
     nx1 = s4_[l1 ? lane + NT : WCH - 1];                                         \
   } while (0)
   if (nr > 0 && fast(g_lo)) SI_PREFETCH(g_lo);
 
   for (int r = 0; r < nr; ++r) {
-    const int64_t g0 = g_lo + R * r;
-    const int64_t base = 160 * g0 - 8;
+    const int g0 = g_lo + R * r;
+    const int base = 160 * g0 + soff - 8;
     const bool fr = fast(g0);
     lds_order();   // the previous round's reads of win / z are issued
     if (fr) {
@@ -249,8 +262,8 @@ __global__ void __launch_bounds__(NT, 2) si_fe_kernel(SiFeArgs a) {
 #pragma unroll
       for (int j = 0; j < SPL; ++j) {
         const int w = lane + NT * j;
-        const int64_t i = base + w;
-        v[j] = (w < WIN && i >= 0 && i < len) ? x[i] : (int16_t)0;
+        const int i = base + w;
+        v[j] = (w < WIN && i >= 0 && i < lenw) ? xw[i] : (int16_t)0;
       }
 #pragma unroll
       for (int j = 0; j < SPL; ++j)
@@ -262,7 +275,7 @@ __global__ void __launch_bounds__(NT, 2) si_fe_kernel(SiFeArgs a) {
     // ---- pass A: z[n] = s[2n] + i s[2n+1], n = 16 n1 + q (< 200: 400-sample frame in 512) ----------
     {
       const uint32_t* wv = reinterpret_cast<const uint32_t*>(win_of(sm)) + 4 + 80 * fq + q;
-      const int64_t lim = len - (160 * (g0 + fq) + 2 * q);   // s[2n] exists iff 32 n1 < lim
+      const int lim = lenw - (160 * (g0 + fq) + soff + 2 * q);   // s[2n] exists iff 32 n1 < lim
       cd v[16];
       double e2 = 0.0;
       auto load = [&](int n1, bool gated) {
@@ -398,9 +411,9 @@ __global__ void __launch_bounds__(NT, 2) si_fe_kernel(SiFeArgs a) {
       } else {
         v = L[26];
       }
-      const int64_t g = g0 + dcf;
+      const int g = g0 + dcf;
       if (g < g_hi) {
-        const int lf = (int)(g - lbase);
+        const int lf = g - lbase;
         if (lf >= HALO && lf < HALO + OUTF) out[(lf - HALO) * ldf + dcc] = (float)v;
         else sm.ext[lf < HALO ? lf : lf - OUTF][dcc] = (float)v;
       }
@@ -418,7 +431,7 @@ __global__ void __launch_bounds__(NT, 2) si_fe_kernel(SiFeArgs a) {
     const int e = lane + NT * i;
     if (e < NL * 13) {
       const int lf = e / 13, c = e - lf * 13;
-      const int64_t g = lbase + lf;
+      const int g = lbase + lf;
       if (g >= g_lo && g < g_hi)
         C[e] = (lf >= HALO && lf < HALO + OUTF) ? out[(lf - HALO) * ldf + c]
                                                 : sm.ext[lf < HALO ? lf : lf - OUTF][c];
@@ -427,11 +440,11 @@ __global__ void __launch_bounds__(NT, 2) si_fe_kernel(SiFeArgs a) {
   lds_order();
   // delta(feat, 2) (speaker_identification.py:141-151): edge padding clamps to the TRUE sequence
   // [0, T - 1]; delta-delta is the delta of the delta sequence, edge-padded again
-  auto cv = [&](int64_t g, int c) {
+  auto cv = [&](int g, int c) {
     g = g < 0 ? 0 : (g > T - 1 ? T - 1 : g);
-    return (double)C[(int)(g - lbase) * 13 + c];
+    return (double)C[(g - lbase) * 13 + c];
   };
-  auto dl = [&](int64_t g, int c) {
+  auto dl = [&](int g, int c) {
     g = g < 0 ? 0 : (g > T - 1 ? T - 1 : g);
     return (-2.0 * cv(g - 2, c) - cv(g - 1, c) + cv(g + 1, c) + 2.0 * cv(g + 2, c)) * 0.1;
   };
@@ -440,7 +453,7 @@ __global__ void __launch_bounds__(NT, 2) si_fe_kernel(SiFeArgs a) {
   for (int i = 0; i < EPL; ++i) {
     const int e = lane + NT * i;
     const int t = e / 13, c = e - t * 13;
-    const int64_t g = frame0 + t;
+    const int g = lbase + HALO + t;   // frame0 + t, window-relative
     float* o = out + t * ldf + c;
     if (ldf == 40 && c == 12) o[27] = 0.0f;   // the pad column 39 (t * 40 + 39)
     float v0 = 0.0f, v1 = 0.0f, v2 = 0.0f;
