@@ -12,7 +12,7 @@ import os
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-STAGE_KERNELS = {'conv': ('resblk_kernel', 'conv_h3_kernel', 'conv_kernel', 'siu_kernel'),
+STAGE_KERNELS = {'conv': ('resblk_kernel', 'conv_h3_kernel', 'conv_kernel', 'siu_kernel', 'odu_kernel'),
                  'od_fe': ('od_fe_kernel', 'od_fe3_kernel'),
                  'nr': ('nr_stft_kernel', 'nr_gmax_kernel', 'nr_rows_kernel', 'nr_gate_kernel', 'nr_ola_kernel')}
 PAIRS = [('od_pipeline', 'od_pipeline_kernel_stats'), ('si_pipeline', 'si_pipeline_kernel_stats'),
