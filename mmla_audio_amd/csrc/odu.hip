@@ -90,11 +90,15 @@ __global__ void __launch_bounds__(64 * NW, MINW) odu_kernel(OduArgs a) {
   static_assert(POOL || CIN == C, "residual blocks keep their width");
   constexpr int TLW = (W + TW - 1) / TW;
   constexpr int XP = TW + 2, XH = H + 2, NXP = XH * XP;   // x halo: rows -1 .. H, columns -1 .. TW
-  constexpr int LDX = CK + 8;                             // fp16 per staged x pixel (16-B pad)
-  // fp16 per halo row: padded so that GEMM a's 16-lane ds_read_b128 groups (8 rows x 2 columns at
-  // TW 2, 4 x 4 at TW 4) hit 64 distinct banks -- 352 / 576 B instead of 320 / 480 (2-way conflicts;
-  // the LDS plane of every instantiation keeps its size: t1 or the LDS limit per CU bound it)
-  constexpr int XRP = TW == 2 ? 176 : TW == 4 ? 288 : XP * LDX;
+  // x halo layout, chosen so GEMM a's 16-lane ds_read_b128 groups (8 rows x 2 columns at TW 2, 4 x 4
+  // at TW 4) hit 64 distinct banks (tools: the guide's lane groups, MI355X_MICROARCH.md section LDS):
+  //   TW 2: 64-B pixels (no pad), 288-B rows, the two 16-B halves of each 32-B k-step swapped in odd
+  //         halo columns -- conflict-free reads AND staging stores at 38 KB for block 4's halo, so its
+  //         LDS plane (t1, 38.6 KB) admits four workgroups per CU (42.2 KB with 80-B pixels: three);
+  //   TW 4: 80-B pixels (16-B pad), 576-B rows instead of 480 (2-way conflicts), same plane size.
+  constexpr int LDX = TW == 2 ? CK : CK + 8;              // fp16 per staged x pixel
+  constexpr int XRP = TW == 2 ? 144 : TW == 4 ? 288 : XP * LDX;   // fp16 per halo row
+  constexpr bool XSW = TW == 2;                           // odd-column half swap
   constexpr int T1R = H + 3, NT1 = T1R * TW;              // t1 rows -1 .. H + 1 (three zero rows)
   constexpr int LDT = C + 8;                              // fp16 per t1 pixel
   constexpr int PLANE = XH * XRP > NT1 * LDT ? XH * XRP : NT1 * LDT;
@@ -133,6 +137,9 @@ __global__ void __launch_bounds__(64 * NW, MINW) odu_kernel(OduArgs a) {
     const __amdgpu_buffer_rsrc_t rh = odu_rsrc(a.wah), rl = odu_rsrc(a.wal);
     constexpr size_t tap_stride = (size_t)C * CIN;
     const int q = tid % QPP;
+    // XSW: this lane's k-half offset in an even / odd halo column (m % TW = lane & 1 at TW 2)
+    const int kx0 = XSW ? 8 * ((lane >> 5) ^ (lane & 1)) : koff;
+    const int kx1 = XSW ? 8 * ((lane >> 5) ^ (lane & 1) ^ 1) : koff;
 #pragma unroll 1
     for (int ch = 0; ch < NCHX; ++ch) {
       if (ch > 0) __syncthreads();   // every wave is done reading the previous chunk
@@ -174,7 +181,8 @@ __global__ void __launch_bounds__(64 * NW, MINW) odu_kernel(OduArgs a) {
         f16x4 hv, lv;
         split4(v, hv, lv);
         const int px = task / QPP;
-        const int xo = (px / XP) * XRP + (px % XP) * LDX + 4 * q;
+        const int cx = px % XP;
+        const int xo = (px / XP) * XRP + cx * LDX + (XSW ? 8 * ((q >> 1) ^ (cx & 1)) + 4 * (q & 1) : 4 * q);
         *reinterpret_cast<f16x4*>(lhi + xo) = hv;
         *reinterpret_cast<f16x4*>(llo + xo) = lv;
       }
@@ -196,7 +204,7 @@ __global__ void __launch_bounds__(64 * NW, MINW) odu_kernel(OduArgs a) {
 #pragma unroll
           for (int mt = 0; mt < MT; ++mt) {
             const int m = mpix[mt];
-            const int off = (m / TW + dy) * XRP + (m % TW + dx) * LDX + 16 * s + koff;
+            const int off = (m / TW + dy) * XRP + (m % TW + dx) * LDX + 16 * s + (dx & 1 ? kx1 : kx0);
             const f16x8 ah = *reinterpret_cast<const f16x8*>(lhi + off);
             const f16x8 al = *reinterpret_cast<const f16x8*>(llo + off);
             acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(bl[s], ah, acc[mt], 0, 0, 0);
@@ -421,7 +429,7 @@ hipError_t odu_launch(const OduArgs& a, int h, int w, int cin, int c, bool pool,
   // blocks 5-6 TW 4 at 3 waves per SIMD (<= 168 VGPRs, 1 spilled) 8.56 -> 7.55 ms; TW 2 with two-wave
   // workgroups 8.16 ms; 4 waves per SIMD (<= 128 VGPRs) spill 20-44 VGPRs: block 7 15.5 -> 17.2 ms,
   // blocks 5-6 10.6 ms.  Blocks 4 and 8-9 are LDS-bound at 3 workgroups per CU (42 / 41 KB)
-  if (h == 64 && pool) return launch<64, 76, 32, 64, 2, true>(a, s);
+  if (h == 64 && pool) return launch<64, 76, 32, 64, 2, true, 4, 4>(a, s);
   if (h == 32 && c == 64) return launch<32, 38, 64, 64, 4, false, 4, 3>(a, s);
   if (h == 32 && pool) return launch<32, 38, 64, 128, 2, true>(a, s);
   return launch<16, 19, 128, 128, 4, false>(a, s);
