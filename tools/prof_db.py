@@ -15,7 +15,11 @@ def load(path):
 
 
 def main():
-    args = [a for a in sys.argv[1:] if not a.startswith('--')]
+    argv = sys.argv[1:]
+    if '--csv' in argv:   # its value is an output path, not a baseline
+        i = argv.index('--csv')
+        argv = argv[:i] + argv[i + 2:]
+    args = [a for a in argv if not a.startswith('--')]
     cur = load(args[0])
     base = load(args[1]) if len(args) > 1 else {}
     if '--csv' in sys.argv:
