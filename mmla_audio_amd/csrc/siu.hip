@@ -45,8 +45,8 @@ MMLA_DEV float bn_relu(float v, float sc, float sh) { return fmaxf(fmaf(v, sc, s
 // FIN (the last unit): the epilogue writes BN + ReLU + AveragePooling1D(4) of the unit's output
 // (speaker_identification.py:208-212, nets.hip bn_relu_avgpool4_kernel's arithmetic) instead of the
 // output itself; tiles then hold a multiple of 4 output rows, so no pool window straddles two
-template <int CIN, int C, int ROWS, int NW, bool POOL, bool FIN>
-__global__ void __launch_bounds__(64 * NW, 2) siu_kernel(SiuArgs a) {
+template <int CIN, int C, int ROWS, int NW, bool POOL, bool FIN, int MINW = 2>
+__global__ void __launch_bounds__(64 * NW, MINW) siu_kernel(SiuArgs a) {
   constexpr int NT = 64 * NW;
   constexpr int WN = C / 32;           // waves along N (32 columns each), as conv_h3 with BN = C
   constexpr int WM = NW / WN;
@@ -322,12 +322,12 @@ __global__ void __launch_bounds__(64 * NW, 2) siu_kernel(SiuArgs a) {
   if (rbad && a.range_flag) *a.range_flag = 1;
 }
 
-template <int CIN, int C, int ROWS, int NW, bool POOL = false, bool FIN = false>
+template <int CIN, int C, int ROWS, int NW, bool POOL = false, bool FIN = false, int MINW = 2>
 hipError_t launch(const SiuArgs& a, hipStream_t s) {
   constexpr int R = FIN ? (ROWS - 2) / 4 * 4 : ROWS - 2;
   const int64_t rows = (int64_t)a.n * a.t;
   const int64_t blocks = (rows + R - 1) / R;
-  hipLaunchKernelGGL((siu_kernel<CIN, C, ROWS, NW, POOL, FIN>), dim3((unsigned)blocks), dim3(64 * NW), 0, s, a);
+  hipLaunchKernelGGL((siu_kernel<CIN, C, ROWS, NW, POOL, FIN, MINW>), dim3((unsigned)blocks), dim3(64 * NW), 0, s, a);
   return hipGetLastError();
 }
 
@@ -345,8 +345,11 @@ hipError_t sipu_launch(const SiuArgs& a, int cin, int c, hipStream_t s) {
   if ((int64_t)a.n * a.t == 0) return hipSuccess;
   if (!a.x || !a.y || a.x == a.y || a.t < 1 || a.t != (a.t_src + 1) / 2 || !a.wsh || !a.wsl || !a.bs)
     return hipErrorInvalidValue;
+  // unit 4 (32 -> 64 channels): 128-row tiles at 3 waves per SIMD (112 VGPRs, 37.7 KB) instead of
+  // 256-row tiles at 2 (152 VGPRs, 74.6 KB): SI +1.1 % (A/B, 2 rounds; the same choice for the other
+  // units -- C 32 pool / non-pool at 128 rows and 4 waves per SIMD, C 64 at 128 rows -- was neutral)
   if (cin == 32 && c == 32) return launch<32, 32, 256, 4, true>(a, s);
-  if (cin == 32 && c == 64) return launch<32, 64, 256, 4, true>(a, s);
+  if (cin == 32 && c == 64) return launch<32, 64, 128, 4, true, false, 3>(a, s);
   if (cin == 64 && c == 128) return launch<64, 128, 128, 4, true>(a, s);
   return hipErrorInvalidValue;
 }
