@@ -350,7 +350,9 @@ hipError_t sipu_launch(const SiuArgs& a, int cin, int c, hipStream_t s) {
   // units -- C 32 pool / non-pool at 128 rows and 4 waves per SIMD, C 64 at 128 rows -- was neutral)
   if (cin == 32 && c == 32) return launch<32, 32, 256, 4, true>(a, s);
   if (cin == 32 && c == 64) return launch<32, 64, 128, 4, true, false, 3>(a, s);
-  if (cin == 64 && c == 128) return launch<64, 128, 128, 4, true>(a, s);
+  // unit 7 (64 -> 128): 64-row tiles at 3 waves per SIMD (158 VGPRs) instead of 128-row tiles at 2
+  // (227): SI +1.0 % (A/B, 2 rounds; 64-row tiles for units 8 / 9 at 3 waves: +0.1-0.6 % / noise)
+  if (cin == 64 && c == 128) return launch<64, 128, 64, 4, true, false, 3>(a, s);
   return hipErrorInvalidValue;
 }
 
