@@ -109,24 +109,16 @@ struct Geo {
   // discarded result), cols w0-1 .. w0+TW
   static constexpr int XR = TR + 2, XC = TW + 2, XNP = XR * XC;
   // LDS pixel layouts.  ds_read_b128 of a 16 x 32 fragment (lanes = 16 consecutive pixels x 4
-  // 16-B k-groups; MI355X_MICROARCH.md LDS lane groups): 16 channels -> separate hi / lo planes of
-  // 32-B pixels (stride 32 mod 64 B: conflict-free).  32 channels (the block 2-3 halo, every t1) ->
-  // one 128-B pixel holding eight 16-B chunks, hi k-groups 0-3 then lo 4-7, chunk c stored at
-  // c ^ (pixel column & 7): a group's 16 lanes (8 columns x hi k-groups 0 / 1 at either column
-  // parity) then cover all 64 banks, as the round-4 160-B padded pixels did, in 20 % less LDS --
-  // which is what lets blocks 2-3 run three workgroups per CU (48 KB).  The lo chunk of a hi chunk
-  // is at offset ^ 32 (halves).
-  static constexpr bool CX = CIN == 32;            // 128-B swizzled halo pixels
-  static constexpr int XPS = CIN == 16 ? 16 : 2 * CIN;                 // halfs per pixel
-  static constexpr int XLO = CIN == 16 ? XNP * 16 : 0;       // lo offset from hi (CX: the ^ 32)
+  // 16-B k-groups) is conflict-free when the pixel stride is 32 mod 64 bytes
+  // (MI355X_MICROARCH.md LDS lane groups): 16 channels -> separate hi / lo planes of 32-B pixels;
+  // 32 channels -> hi and lo interleaved in one 160-B pixel (64 + 64 + 32 pad).
+  static constexpr int XPS = CIN == 16 ? 16 : (2 * CIN + 16 + 31) / 32 * 32 - 16;   // halfs
+  static constexpr int XLO = CIN == 16 ? XNP * 16 : CIN;     // lo offset from hi (halfs)
   static constexpr int XREG = CIN == 16 ? 2 * XNP * 16 : XNP * XPS;
-  static constexpr int TPS = 2 * C;                // t1: 128-B swizzled pixels as above
-  static_assert(C == 32 && (CIN == 16 || CIN == 32), "layouts assume 16 / 32 input and 32 output channels");
+  static constexpr int TPS = (2 * C + 16 + 31) / 32 * 32 - 16;   // t1: interleaved hi | lo | pad
+  static constexpr int TLO = C;
   static constexpr int TREG = TRP * TW * TPS;
-  // (+ one halo row for CX: GEMM 1's padded t1 row reads one row past the halo -- finite LDS data
-  // whose result is discarded; the 16-channel layout's reads past it land in its lo plane / t1)
-  static constexpr int XREGR = CX ? XREG + XC * XPS : XREG;
-  static constexpr int SM = XREGR > TREG ? XREGR : TREG;
+  static constexpr int SM = XREG > TREG ? XREG : TREG;
   static constexpr int MT1 = TRP / WM;             // t1 rows per wave (GEMM 1)
   static constexpr int MT2 = TH / WM;              // output rows per wave (GEMM 2)
   static constexpr int KS1 = (9 * CIN + 31) / 32;  // GEMM 1 k-steps
@@ -138,12 +130,9 @@ struct Geo {
   // LDS (51 KB) admits a third workgroup per CU: conv 1432 -> 1386 ms per OD step (A/B).  (With
   // the [co][k] rows and no prefetch the same move had been 7.5 % slower.)  Blocks 2-3 keep them in
   // LDS: without them they still need 60 KB, two workgroups per CU.
-  // (round 5: blocks 2-3 too -- with the 128-B halo pixels their LDS is 48 KB, three workgroups
-  // per CU; the residual is re-read from HBM / L2 in the epilogue, so the staged halo's registers
-  // are free after the staging: <= 168 VGPRs)
-  static constexpr bool W2LDS = false;
+  static constexpr bool W2LDS = CIN != 16 && TH == 16;
   static constexpr int W2 = W2LDS ? C * LW2 : 0;
-  static constexpr int MINB = 3;               // resident workgroups per CU
+  static constexpr int MINB = W2LDS ? 2 : 3;   // resident workgroups per CU
   static constexpr int PF = 3;                     // GEMM 1 B fragments in flight (k-steps)
   static constexpr int QPP = CIN / 4;              // float4 per halo pixel
   static constexpr int MAXT = (XNP * QPP + NT - 1) / NT;
@@ -387,14 +376,8 @@ __global__ void __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(R
       split2(v23, h23, l23);
       const f16x4 hv = {h01.x, h01.y, h23.x, h23.y};
       const f16x4 lv = {l01.x, l01.y, l23.x, l23.y};
-      if constexpr (G::CX) {
-        const int o = px * XPS + 8 * ((q >> 1) ^ ((px % XC) & 7)) + 4 * (q & 1);
-        *reinterpret_cast<f16x4*>(smem + o) = hv;
-        *reinterpret_cast<f16x4*>(smem + (o ^ 32)) = lv;
-      } else {
-        *reinterpret_cast<f16x4*>(smem + px * XPS + 4 * q) = hv;
-        *reinterpret_cast<f16x4*>(smem + px * XPS + G::XLO + 4 * q) = lv;
-      }
+      *reinterpret_cast<f16x4*>(smem + px * XPS + 4 * q) = hv;
+      *reinterpret_cast<f16x4*>(smem + px * XPS + G::XLO + 4 * q) = lv;
     }
   }
   __syncthreads();
@@ -438,13 +421,6 @@ __global__ void __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(R
   {
     const _Float16* ahb = smem + (wm * MT1 * XC + col) * XPS;   // + m * XC * XPS (immediate)
     const _Float16* alb = ahb + G::XLO;
-    // CX: this lane's hi / lo chunk offsets in halo columns col + dx (the pixel base is 64-aligned)
-    int swh[3], swl[3];
-#pragma unroll
-    for (int d = 0; d < 3; ++d) {
-      swh[d] = 8 * (grp ^ ((col + d) & 7));
-      swl[d] = swh[d] ^ 32;
-    }
 #pragma unroll
     for (int s = 0; s < KS1; ++s) {
       const int kk = 32 * s + 8 * grp;
@@ -452,8 +428,7 @@ __global__ void __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(R
       const int ci = kk - tap * CIN;
       tap = tap > 8 ? 8 : tap;                 // k >= 9 * CIN: zero weights, any finite A
       const int dy = tap / 3, dx = tap - (tap / 3) * 3;
-      const int koff = (dy * XC + dx) * XPS + (G::CX ? 0 : ci);
-      const int kh = G::CX ? koff + swh[dx] : koff, kl = G::CX ? koff + swl[dx] : koff;
+      const int koff = (dy * XC + dx) * XPS + ci;
       f16x8 ch[NTW], cl[NTW];
 #pragma unroll
       for (int nt = 0; nt < NTW; ++nt) {
@@ -469,8 +444,8 @@ __global__ void __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(R
       }
 #pragma unroll
       for (int m = 0; m < MT1; ++m) {
-        const f16x8 ah = *reinterpret_cast<const f16x8*>(ahb + kh + m * XC * XPS);
-        const f16x8 al = *reinterpret_cast<const f16x8*>(alb + kl + m * XC * XPS);
+        const f16x8 ah = *reinterpret_cast<const f16x8*>(ahb + koff + m * XC * XPS);
+        const f16x8 al = *reinterpret_cast<const f16x8*>(alb + koff + m * XC * XPS);
 #pragma unroll
         for (int nt = 0; nt < NTW; ++nt) {
           acc1[m][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, cl[nt], acc1[m][nt], 0, 0, 0);
@@ -488,13 +463,11 @@ __global__ void __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(R
   // ---- t1 -> LDS: BN2(acc + b1) + ELU; rows outside the image are the (4,1) conv's zero padding ----
   // BN2(v + b1) = acc * (2^-12 s2) + (b1 s2 + t2): one v_pk_fma_f32 per pixel pair
   {
-    // pixel p = m TW + 4 grp + i: p & 7 = 4 (grp & 1) + i, so channel n sits at chunk
-    // (n >> 3) ^ (4 (grp & 1) + i), i.e. at nb ^ 8 i with nb below; lo at ^ 32
-    _Float16* const thb = smem + wm * MT1 * TW * TPS + 4 * grp * TPS;   // + (m * TW + i) * TPS + ...
+    _Float16* const thb = smem + wm * MT1 * TW * TPS + 4 * grp * TPS;   // + (m * TW + i) * TPS + n
+    _Float16* const tlb = thb + G::TLO;
 #pragma unroll
     for (int nt = 0; nt < NTW; ++nt) {
       const int n = (wn * NTW + nt) * 16 + col;
-      const int nb = 8 * ((n >> 3) ^ (4 * (grp & 1))) + (n & 7);
       const float s2 = ps2[nt];
       const float c2 = fmaf(pb1[nt], s2, pt2[nt]);
       const f32x2 s2v = {s2 * a.u1, s2 * a.u1}, c2v = {c2, c2};
@@ -514,10 +487,10 @@ __global__ void __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(R
           const f32x2 v = u * rmask;
           f16x2 hv, lv;
           split2(v, hv, lv);
-          thb[(m * TW + i) * TPS + (nb ^ (8 * i))] = hv.x;
-          thb[(m * TW + i) * TPS + (nb ^ (8 * i) ^ 32)] = lv.x;
-          thb[(m * TW + i + 1) * TPS + (nb ^ (8 * (i + 1)))] = hv.y;
-          thb[(m * TW + i + 1) * TPS + (nb ^ (8 * (i + 1)) ^ 32)] = lv.y;
+          thb[(m * TW + i) * TPS + n] = hv.x;
+          tlb[(m * TW + i) * TPS + n] = lv.x;
+          thb[(m * TW + i + 1) * TPS + n] = hv.y;
+          tlb[(m * TW + i + 1) * TPS + n] = lv.y;
         }
       }
     }
@@ -533,8 +506,7 @@ __global__ void __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(R
     for (int nt = 0; nt < NTW; ++nt) d1[m][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
   {
     const _Float16* ahb = smem + (wm * MT2 * TW + col) * TPS;
-    // pixel column col (TW = 16: rows keep & 7): hi chunk grp at grp ^ (col & 7), lo at ^ 32
-    const int t2h = 8 * (grp ^ (col & 7)), t2l = t2h ^ 32;
+    const _Float16* alb = ahb + G::TLO;
     const int b2o = ((wn * NTW) * 16 + col) * G::LW2 + 8 * grp;
     // !W2LDS: GEMM 2's B from L2 in fragment order (resblk_split_weights, frag), one k-step ahead
     const int b2g = (wn * NTW) * 512 + lane * 8;   // + nt * 512 + s * (C / 16) * 512
@@ -551,9 +523,7 @@ __global__ void __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(R
     for (int s = 0; s < KS2; ++s) {
       const int kk = 32 * s + 8 * grp;
       const int dy = kk / C, ci = kk - (kk / C) * C;
-      const int koff = dy * TW * TPS;
-      static_assert(C == 32, "k-step s = tap s, ci = 8 grp");
-      (void)ci;
+      const int koff = dy * TW * TPS + ci;
       f16x8 gh[NTW], gl[NTW];
 #pragma unroll
       for (int nt = 0; nt < NTW; ++nt) {
@@ -571,8 +541,8 @@ __global__ void __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(R
       }
 #pragma unroll
       for (int m = 0; m < MT2; ++m) {
-        const f16x8 ah = *reinterpret_cast<const f16x8*>(ahb + koff + t2h + m * TW * TPS);
-        const f16x8 al = *reinterpret_cast<const f16x8*>(ahb + koff + t2l + m * TW * TPS);
+        const f16x8 ah = *reinterpret_cast<const f16x8*>(ahb + koff + m * TW * TPS);
+        const f16x8 al = *reinterpret_cast<const f16x8*>(alb + koff + m * TW * TPS);
 #pragma unroll
         for (int nt = 0; nt < NTW; ++nt) {
           d1[m][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, gl[nt], d1[m][nt], 0, 0, 0);
@@ -659,8 +629,7 @@ __global__ void __launch_bounds__(NT, (Geo<CIN, C, POOL>::MINB)) resblk_kernel(R
       const int oh = h0 + r, ow = w0 + c;
       if (!interior && (oh >= a.h || ow >= a.w)) continue;
       const float4 v = *reinterpret_cast<const float4*>(so + (r * TW + c) * OPS + 4 * q);
-      // the residual re-read (L2: this tile's halo was just loaded) rather than kept in pre[]
-      const float4 x = *reinterpret_cast<const float4*>(a.x + (((int64_t)clip * a.h + oh) * a.w + ow) * CIN + 4 * q);
+      const float4 x = pre[j];
       *reinterpret_cast<float4*>(a.y + (((int64_t)clip * a.h + oh) * a.w + ow) * C + 4 * q) =
           make_float4(v.x + x.x, v.y + x.y, v.z + x.z, v.w + x.w);
     }
