@@ -56,12 +56,17 @@ __device__ __forceinline__ f32x2 elu2(f32x2 u) {
   return f32x2{u.x > 0.0f ? u.x : e.x, u.y > 0.0f ? u.y : e.y};
 }
 
-// v * 2^4 = hi + lo, both fp16 (RNE)
+// v * 2^4 = hi + lo, both fp16 (RNE).  lo = f16(v' - hi) by v_fma_mix: the exact difference rounded
+// once, as cvt(v' - f32(hi)) rounds it (v' - hi is exact in f32) -- bit-identical, 4 VALU per pair
+// instead of 6 (two v_cvt_f32_f16 and a v_pk_add gone); clang keeps the cvt + sub + cvt form itself
 __device__ __forceinline__ void split2(f32x2 v, f16x2& h, f16x2& l) {
   v = v * ACT_SCALE;
   h = __builtin_convertvector(v, f16x2);
-  const f32x2 hf = __builtin_convertvector(h, f32x2);
-  l = __builtin_convertvector(v - hf, f16x2);
+  uint32_t lu;
+  asm("v_fma_mixlo_f16 %0, %1, 1.0, -%2 op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixhi_f16 %0, %3, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+      : "=&v"(lu) : "v"(v.x), "v"(__builtin_bit_cast(uint32_t, h)), "v"(v.y));
+  l = __builtin_bit_cast(f16x2, lu);
 }
 
 // GEMM 1 / GEMM 2 B fragments by raw buffer loads from a wave-uniform descriptor
