@@ -5,6 +5,19 @@
 
 #define MMLA_DEV __device__ __forceinline__
 
+// lo halves of the 3xFP16 split of two scaled values a, b whose hi halves are the f16 pair `hi`
+// (bits 0-15 = f16(a), 16-31 = f16(b)): f16(a - hi.a), f16(b - hi.b) by v_fma_mix -- the exact
+// difference rounded once, bit-identical to cvt(a - f32(hi.a)) (a - hi is exact in f32); two VALU
+// where clang emits cvt + sub + cvt per value.  a, b must be plain VALU results (no MFMA / trans
+// producer hazard is visible to the compiler inside the asm).
+MMLA_DEV uint32_t split_lo2(float a, float b, uint32_t hi) {
+  uint32_t lo;
+  asm("v_fma_mixlo_f16 %0, %1, 1.0, -%2 op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixhi_f16 %0, %3, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+      : "=&v"(lo) : "v"(a), "v"(hi), "v"(b));
+  return lo;
+}
+
 // XCD-aware workgroup order (MI355X_MICROARCH.md, workgroup dispatch): blocks b and b + 8 share an
 // XCD's L2, so the logical id handed to a kernel puts consecutive ids on one XCD -- neighbouring
 // tiles of one clip, whose input halos overlap, then meet in the same L2.  Bijective for any count.

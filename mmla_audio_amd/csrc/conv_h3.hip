@@ -364,10 +364,10 @@ __global__ void __launch_bounds__(NT, (conv_minw<KH, BN, TW, EPI, SHP::FIXED>())
       hv[1] = (_Float16)v.y;
       hv[2] = (_Float16)v.z;
       hv[3] = (_Float16)v.w;
-      lv[0] = (_Float16)(v.x - (float)hv[0]);
-      lv[1] = (_Float16)(v.y - (float)hv[1]);
-      lv[2] = (_Float16)(v.z - (float)hv[2]);
-      lv[3] = (_Float16)(v.w - (float)hv[3]);
+      {
+        const uint2 hu_ = __builtin_bit_cast(uint2, hv);
+        lv = __builtin_bit_cast(f16x4, make_uint2(split_lo2(v.x, v.y, hu_.x), split_lo2(v.z, v.w, hu_.y)));
+      }
       *reinterpret_cast<f16x4*>(lds_hi + px * LDP + q * 4) = hv;
       *reinterpret_cast<f16x4*>(lds_lo + px * LDP + q * 4) = lv;
     }

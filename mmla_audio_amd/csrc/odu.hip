@@ -66,10 +66,8 @@ MMLA_DEV void split4(float4 v, f16x4& h, f16x4& l) {
   h[1] = (_Float16)v.y;
   h[2] = (_Float16)v.z;
   h[3] = (_Float16)v.w;
-  l[0] = (_Float16)(v.x - (float)h[0]);
-  l[1] = (_Float16)(v.y - (float)h[1]);
-  l[2] = (_Float16)(v.z - (float)h[2]);
-  l[3] = (_Float16)(v.w - (float)h[3]);
+  const uint2 hu = __builtin_bit_cast(uint2, h);
+  l = __builtin_bit_cast(f16x4, make_uint2(split_lo2(v.x, v.y, hu.x), split_lo2(v.z, v.w, hu.y)));
 }
 
 MMLA_DEV bool in_range4(float4 v) {

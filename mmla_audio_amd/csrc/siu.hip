@@ -131,10 +131,10 @@ __global__ void __launch_bounds__(64 * NW, MINW) siu_kernel(SiuArgs a) {
         hv[1] = (_Float16)v.y;
         hv[2] = (_Float16)v.z;
         hv[3] = (_Float16)v.w;
-        lv[0] = (_Float16)(v.x - (float)hv[0]);
-        lv[1] = (_Float16)(v.y - (float)hv[1]);
-        lv[2] = (_Float16)(v.z - (float)hv[2]);
-        lv[3] = (_Float16)(v.w - (float)hv[3]);
+        {
+          const uint2 hu_ = __builtin_bit_cast(uint2, hv);
+          lv = __builtin_bit_cast(f16x4, make_uint2(split_lo2(v.x, v.y, hu_.x), split_lo2(v.z, v.w, hu_.y)));
+        }
         const int row = task / QPP;
         *reinterpret_cast<f16x4*>(lhi + row * LDPX + ci) = hv;
         *reinterpret_cast<f16x4*>(llo + row * LDPX + ci) = lv;
