@@ -99,8 +99,14 @@ __global__ void __launch_bounds__(64 * NW, MINW) odu_kernel(OduArgs a) {
   constexpr bool XSW = TW == 2;                           // odd-column half swap
   constexpr int T1R = H + 3, NT1 = T1R * TW;              // t1 rows -1 .. H + 1 (three zero rows)
   constexpr int LDT = C + 8;                              // fp16 per t1 pixel
-  constexpr int PLANE = XH * XRP > NT1 * LDT ? XH * XRP : NT1 * LDT;
   constexpr int NCHX = CIN / CK, NCH = C / CK;
+  // DB: two halo buffers, so chunk ch + 1 is loaded and staged right behind chunk ch's MFMAs (which
+  // run on in the matrix pipe) instead of after a barrier; only where the second buffer fits inside
+  // the t1 plane the LDS already holds (blocks 7, 8-9; blocks 5-6 would drop to two workgroups per CU)
+  constexpr bool DB = NCHX > 1 && C == 128;
+  constexpr int XBUF = XH * XRP;                          // fp16 per halo buffer and plane
+  constexpr int XTOT = DB ? 2 * XBUF : XBUF;
+  constexpr int PLANE = XTOT > NT1 * LDT ? XTOT : NT1 * LDT;
   constexpr int QPP = CK / 4;                             // float4 per pixel and chunk
   constexpr int MAXT = (NXP * QPP + NT - 1) / NT;
   static_assert(NT % QPP == 0, "a thread's channel quad is fixed");
@@ -138,9 +144,8 @@ __global__ void __launch_bounds__(64 * NW, MINW) odu_kernel(OduArgs a) {
     // XSW: this lane's k-half offset in an even / odd halo column (m % TW = lane & 1 at TW 2)
     const int kx0 = XSW ? 8 * ((lane >> 5) ^ (lane & 1)) : koff;
     const int kx1 = XSW ? 8 * ((lane >> 5) ^ (lane & 1) ^ 1) : koff;
-#pragma unroll 1
-    for (int ch = 0; ch < NCHX; ++ch) {
-      if (ch > 0) __syncthreads();   // every wave is done reading the previous chunk
+    // global loads of chunk ch's halo quads, then BN_in + ELU + 2^4 + split into halo buffer buf
+    auto load_stage = [&](int ch, int buf) {
       const int ci = ch * CK + 4 * q;
       const float4 sc = *reinterpret_cast<const float4*>(a.s_in + ci);
       const float4 sh = *reinterpret_cast<const float4*>(a.t_in + ci);
@@ -156,13 +161,6 @@ __global__ void __launch_bounds__(64 * NW, MINW) odu_kernel(OduArgs a) {
           pre[j] = *reinterpret_cast<const float4*>(xc + ((int64_t)ih * W + iw) * CIN + ci);
           valid |= 1u << j;
         }
-      }
-      // tap 0's B fragments, in flight across the staging
-      f16x8 bh[KS], bl[KS];
-#pragma unroll
-      for (int s = 0; s < KS; ++s) {
-        bh[s] = odu_frag(rh, (size_t)(ch * KS + s) * kstr, lofs);
-        bl[s] = odu_frag(rl, (size_t)(ch * KS + s) * kstr, lofs);
       }
 #pragma unroll
       for (int j = 0; j < MAXT; ++j) {
@@ -181,10 +179,29 @@ __global__ void __launch_bounds__(64 * NW, MINW) odu_kernel(OduArgs a) {
         const int px = task / QPP;
         const int cx = px % XP;
         const int xo = (px / XP) * XRP + cx * LDX + (XSW ? 8 * ((q >> 1) ^ (cx & 1)) + 4 * (q & 1) : 4 * q);
-        *reinterpret_cast<f16x4*>(lhi + xo) = hv;
-        *reinterpret_cast<f16x4*>(llo + xo) = lv;
+        *reinterpret_cast<f16x4*>(lhi + buf * XBUF + xo) = hv;
+        *reinterpret_cast<f16x4*>(llo + buf * XBUF + xo) = lv;
       }
+    };
+    if constexpr (DB) {
+      load_stage(0, 0);
       __syncthreads();
+    }
+#pragma unroll 1
+    for (int ch = 0; ch < NCHX; ++ch) {
+      const int buf = DB ? (ch & 1) : 0;
+      // tap 0's B fragments, in flight across the staging
+      f16x8 bh[KS], bl[KS];
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        bh[s] = odu_frag(rh, (size_t)(ch * KS + s) * kstr, lofs);
+        bl[s] = odu_frag(rl, (size_t)(ch * KS + s) * kstr, lofs);
+      }
+      if constexpr (!DB) {
+        if (ch > 0) __syncthreads();   // every wave is done reading the previous chunk
+        load_stage(ch, 0);
+        __syncthreads();
+      }
 #pragma unroll
       for (int tap = 0; tap < 9; ++tap) {
         const int dy = tap / 3, dx = tap - (tap / 3) * 3;
@@ -202,7 +219,7 @@ __global__ void __launch_bounds__(64 * NW, MINW) odu_kernel(OduArgs a) {
 #pragma unroll
           for (int mt = 0; mt < MT; ++mt) {
             const int m = mpix[mt];
-            const int off = (m / TW + dy) * XRP + (m % TW + dx) * LDX + 16 * s + (dx & 1 ? kx1 : kx0);
+            const int off = buf * XBUF + (m / TW + dy) * XRP + (m % TW + dx) * LDX + 16 * s + (dx & 1 ? kx1 : kx0);
             const f16x8 ah = *reinterpret_cast<const f16x8*>(lhi + off);
             const f16x8 al = *reinterpret_cast<const f16x8*>(llo + off);
             acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(bl[s], ah, acc[mt], 0, 0, 0);
@@ -215,6 +232,14 @@ __global__ void __launch_bounds__(64 * NW, MINW) odu_kernel(OduArgs a) {
             bh[s] = nbh[s];
             bl[s] = nbl[s];
           }
+        }
+      }
+      if constexpr (DB) {
+        if (ch + 1 < NCHX) {
+          // buffer (ch + 1) & 1 was last read in chunk ch - 1, whose readers all passed the barrier
+          // that ended that chunk; this chunk's MFMAs are issued and run on meanwhile
+          load_stage(ch + 1, buf ^ 1);
+          __syncthreads();
         }
       }
     }
