@@ -18,6 +18,8 @@
 // without them the same co-run is bit-exact and the kernel is 7-12 % faster.
 // (A per-kernel target attribute is not enough: the HIP headers' helpers, e.g. float2's constructor
 // and threadIdx, then stop inlining across the feature mismatch and spill to scratch.)
+// (Round 5: the MFMA kernel below assembles identically with and without the flag -- it emits no
+// packed-FP32 instruction either way; the flag guards future edits.)
 //
 // Accumulation is float32 (the reference runs the FFT in float64 and stores complex64; the measured
 // deviation on the normalised log-mel is ~1e-5, tolerance 1e-4).  The scalar steps
