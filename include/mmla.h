@@ -64,6 +64,14 @@ int mmla_abi_version(void);
  * tf.keras.models.load_model at record_on_pc.py:88 / SI record_on_pc.py:77). */
 int mmla_crc32c(const void* data, int64_t n, uint32_t* crc);
 
+/* PNG scanline reconstruction (host only, no context or device): `raw` is the inflated IDAT stream
+ * of a non-interlaced image, h rows of 1 filter-type byte + row_bytes bytes; `bpp` = bytes per
+ * complete pixel (>= 1; 1 for sub-byte depths).  Undoes filters 0-4 (None, Sub, Up, Average, Paeth;
+ * PNG spec section 9) into out[h * row_bytes].  MMLA_E_INVALID on an unknown filter type.  Replaces
+ * libpng's row reconstruction inside tf.image.decode_png (record_on_pc.py:157,
+ * overlap_detection_post_processing.py:205; mmla_audio_amd/tf_compat/image.py). */
+int mmla_png_unfilter(const uint8_t* raw, int64_t h, int64_t row_bytes, int32_t bpp, uint8_t* out);
+
 /* Create a context on HIP device `device` (owns a stream, device workspaces and loaded weights). */
 int mmla_create(int device, mmla_ctx** out);
 int mmla_destroy(mmla_ctx* ctx);

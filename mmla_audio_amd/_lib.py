@@ -37,6 +37,7 @@ SIGNATURES = {
     'mmla_nr_reduce': [_P, _P, _I64, _I64, _I64, _P, ctypes.c_uint32],
     'mmla_abi_version': [],
     'mmla_crc32c': [_P, _I64, ctypes.POINTER(_U32)],
+    'mmla_png_unfilter': [_P, _I64, _I64, _I32, _P],
     'mmla_create': [ctypes.c_int, ctypes.POINTER(_P)],
     'mmla_destroy': [_P],
     'mmla_set_stream': [_P, _P],
@@ -113,6 +114,22 @@ def crc32c(data):
     if rc != MMLA_OK:
         raise MmlaError(f'mmla_crc32c: {_ERRORS.get(rc, rc)}', rc)
     return out.value
+
+
+def png_unfilter(raw, h, row_bytes, bpp):
+    """PNG scanline reconstruction (mmla_png_unfilter; host only, no device needed): the inflated
+    IDAT bytes of h rows -> uint8 [h, row_bytes]."""
+    lib = load_library()
+    buf = np.frombuffer(memoryview(raw).cast('B'), np.uint8)
+    if buf.size != h * (row_bytes + 1):
+        raise ValueError(f'PNG image data holds {buf.size} bytes, expected {h} rows of '
+                         f'{row_bytes + 1}')
+    out = np.empty((h, row_bytes), np.uint8)
+    rc = lib.mmla_png_unfilter(buf.ctypes.data if buf.size else None, h, row_bytes, bpp,
+                               out.ctypes.data if out.size else None)
+    if rc != MMLA_OK:
+        raise ValueError('PNG image data: unknown scanline filter type')
+    return out
 
 
 def _ptr(a):

@@ -154,11 +154,15 @@ class AudioSegment:
         """audioop.rms(data, 2): (unsigned int) sqrt(sum(x^2) / n) with a float64 running sum,
         accumulated sample by sample in order as CPython's loop does (np.add.accumulate is that
         sequential loop; np.sum's pairwise sum and an exact int64 sum differ from it once the sum
-        passes 2^53, i.e. after ~8.4 M full-scale samples)"""
+        passes 2^53, i.e. after ~8.4 M full-scale samples).  Chunks of 2^20 samples carry the running
+        sum, so memory stays O(chunk) for hour-long files with the same summation order."""
         if self.data.size == 0:
             return 0
-        x = self.data.astype(np.float64)
-        total = float(np.add.accumulate(x * x)[-1])
+        flat = self.data.reshape(-1)
+        total = 0.0
+        for i in range(0, flat.size, 1 << 20):
+            c = flat[i:i + (1 << 20)].astype(np.float64)
+            total = float(np.add.accumulate(np.concatenate(([total], c * c)))[-1])
         return int(np.sqrt(total / self.data.size))
 
     max_possible_amplitude = 2 ** 15

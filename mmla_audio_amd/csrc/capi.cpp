@@ -145,7 +145,8 @@ struct mmla_ctx {
   bool lstm_split = true;
   // measured (tools/lat_split_sweep.py): OD 1.62 -> 1.53 ms at 128 clips, even at 192, +1 % at 256
   int lstm_split_max = 128;   // env MMLA_LSTM_SPLIT_MAX (A/B; the kernel takes up to 256)
-  // test hook (env MMLA_DEBUG_LSTM_SPIN at create): the split BiLSTM's wait bound in polls (0 = default)
+  // test hook (env MMLA_DEBUG_LSTM_SPIN at create): the split BiLSTM's wait bound in polls (0 = default,
+  // < 0 = give up at the first wait)
   int lstm_spin = 0;
   // 3xFP16 range guard: kernels set range_dev[0] (device-pointer calls; sticky until
   // mmla_range_check) or range_dev[1] (host-pointer micro-batches: re-run in exact f32) when an
@@ -1258,6 +1259,48 @@ int mmla_crc32c(const void* data, int64_t n, uint32_t* crc) {
   return MMLA_OK;
 }
 
+int mmla_png_unfilter(const uint8_t* raw, int64_t h, int64_t row_bytes, int32_t bpp, uint8_t* out) {
+  if (h < 0 || row_bytes < 0 || bpp < 1 || bpp > 8 || ((!raw || !out) && h * row_bytes > 0))
+    return MMLA_E_INVALID;
+  const uint8_t* prev = nullptr;  // row above (all zero for the first row)
+  for (int64_t r = 0; r < h; ++r) {
+    const uint8_t* in = raw + r * (row_bytes + 1);
+    uint8_t* cur = out + r * row_bytes;
+    const int ft = in[0];
+    ++in;
+    switch (ft) {
+      case 0:
+        memcpy(cur, in, (size_t)row_bytes);
+        break;
+      case 1:  // Sub
+        for (int64_t i = 0; i < row_bytes; ++i)
+          cur[i] = (uint8_t)(in[i] + (i >= bpp ? cur[i - bpp] : 0));
+        break;
+      case 2:  // Up
+        for (int64_t i = 0; i < row_bytes; ++i) cur[i] = (uint8_t)(in[i] + (prev ? prev[i] : 0));
+        break;
+      case 3:  // Average (floor of the 9-bit sum)
+        for (int64_t i = 0; i < row_bytes; ++i) {
+          const int a = i >= bpp ? cur[i - bpp] : 0, b = prev ? prev[i] : 0;
+          cur[i] = (uint8_t)(in[i] + ((a + b) >> 1));
+        }
+        break;
+      case 4:  // Paeth
+        for (int64_t i = 0; i < row_bytes; ++i) {
+          const int a = i >= bpp ? cur[i - bpp] : 0, b = prev ? prev[i] : 0;
+          const int c = (prev && i >= bpp) ? prev[i - bpp] : 0;
+          const int p = a + b - c, pa = abs(p - a), pb = abs(p - b), pc = abs(p - c);
+          cur[i] = (uint8_t)(in[i] + ((pa <= pb && pa <= pc) ? a : (pb <= pc ? b : c)));
+        }
+        break;
+      default:
+        return MMLA_E_INVALID;
+    }
+    prev = cur;
+  }
+  return MMLA_OK;
+}
+
 int mmla_create(int device, mmla_ctx** out) {
   if (!out) return MMLA_E_INVALID;
   *out = nullptr;
@@ -1638,12 +1681,14 @@ static int od_features_common(mmla_ctx* c, const T* pcm, int64_t n, int64_t stri
     return fail(c, MMLA_E_INVALID, "bad pcm args");
   HIPCHK(c, hipSetDevice(c->device));
   const bool dev = flags & MMLA_DEVICE_PTR;
-  if constexpr (std::is_same<T, float>::value) {
-    // the front-end splits y 2^3 into fp16 hi + lo: host samples are checked here (what the kernel
-    // reads: the first min(len, 24000) of each clip); device buffers by the kernel into the sticky
-    // range word (mmla_range_check / mmla_synchronize report it)
-    if (!dev && pcm) {
-      for (int64_t i = 0; i < n; ++i) {
+  // float PCM: the front-end splits y 2^3 into fp16 hi + lo, so the kernel checks every sample it
+  // reads (the first min(len, 24000) of each clip) into a range word: device-pointer calls into the
+  // sticky word (mmla_range_check / mmla_synchronize report it), host-pointer calls into their own
+  // word, read after the micro-batch's synchronisation; only then is the micro-batch re-scanned on
+  // the host, to name the first offending sample
+  auto host_range_error = [&](int64_t c0, int64_t cnt) -> int {
+    if constexpr (std::is_same<T, float>::value) {
+      for (int64_t i = c0; i < c0 + cnt; ++i) {
         const int64_t len = std::min<int64_t>(lens ? lens[i] : clip_len, MMLA_OD_CLIP);
         for (int64_t j = 0; j < len; ++j)
           if (!(std::fabs(pcm[i * stride + j]) < 8188.0f))
@@ -1652,14 +1697,17 @@ static int od_features_common(mmla_ctx* c, const T* pcm, int64_t n, int64_t stri
                         "split into fp16)", (long long)i, (long long)j, (double)pcm[i * stride + j]);
       }
     }
-  }
+    return fail(c, MMLA_E_RANGE, "float PCM outside |y| < 8188 in clips %lld..%lld", (long long)c0,
+                (long long)(c0 + cnt - 1));
+  };
   auto body = [&](int64_t c0, int64_t cnt) -> int {
     PcmT<T> p;
     CHK(stage_pcm(c, pcm, c0, cnt, stride, lens, clip_len, MMLA_OD_CLIP, dev, &p));
     OdFeArgs a{};
     if constexpr (std::is_same<T, float>::value) {
       a.pcm_f32 = p.p;
-      a.range_flag = dev ? c->range_dev : nullptr;
+      a.range_flag = dev ? c->range_dev : c->range_dev + 1;
+      if (!dev) HIPCHK(c, hipMemsetAsync(a.range_flag, 0, sizeof(int), c->stream));
     } else {
       a.pcm = p.p;
     }
@@ -1677,6 +1725,11 @@ static int od_features_common(mmla_ctx* c, const T* pcm, int64_t n, int64_t stri
     CHK(copy_back(c, zcr, c0 * OD_W, a.zcr, cnt * OD_W, dev));
     CHK(copy_back(c, img, c0 * OD_IMG, a.img, cnt * OD_IMG, dev));
     if (!dev) HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (std::is_same<T, float>::value && !dev) {
+      int flag = 0;
+      HIPCHK(c, hipMemcpy(&flag, c->range_dev + 1, sizeof(int), hipMemcpyDeviceToHost));
+      if (flag) return host_range_error(c0, cnt);
+    }
     return MMLA_OK;
   };
   if (dev) {   // one launch over the caller's device buffers

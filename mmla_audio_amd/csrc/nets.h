@@ -30,7 +30,7 @@ hipError_t bilstm_h3_launch(const float* seq, int n, int T, int D, const uint16_
 // The same for n <= bilstm_h3_split_max_clips() with each direction's eight hidden-unit groups on
 // eight workgroups per 32 clips (h exchanged through ws between steps; bit-identical).  ws:
 // bilstm_h3_split_ws_bytes() of device memory owned by the stream.  A workgroup that gave up waiting
-// for the others (after `spin` polls; <= 0: the default bound) writes NaN for its units and sets int
+// for the others (after `spin` polls; 0: the default bound; < 0: at the first wait, a test hook) writes NaN for its units and sets int
 // word 63 of ws and *timeout_flag (nullable): the caller must not use that launch's outputs.
 hipError_t bilstm_h3_split_launch(const float* seq, int n, int T, int D, const uint16_t* wfh,
                                   const uint16_t* wfl, const uint16_t* wbh, const uint16_t* wbl,

@@ -572,7 +572,9 @@ __global__ void __launch_bounds__(256, 1) bilstm_h3_split_kernel(const float* __
           __builtin_amdgcn_s_sleep(1);
           ++it;
         }
-        arrived = it < spin || __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= 8 * s;
+        // spin < 0 (test hook): give up at the first wait without polling, deterministically
+        arrived = spin >= 0 &&
+                  (it < spin || __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= 8 * s);
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // pairs with the publishers' release RMW
       }
       __syncthreads();
@@ -828,7 +830,7 @@ hipError_t bilstm_h3_split_launch(const float* seq, int n, int T, int D, const u
                                   int spin, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   if (D != 128 || n > LSTM_SPLIT_TILES * LSTM_SPLIT_ROWS || T < 1) return hipErrorInvalidValue;
-  if (spin <= 0) spin = LSTM_SPLIT_SPIN;
+  if (spin == 0) spin = LSTM_SPLIT_SPIN;   // < 0: the deterministic give-up test hook
   const int tiles = (n + LSTM_SPLIT_ROWS - 1) / LSTM_SPLIT_ROWS;
   int* sync = static_cast<int*>(ws);
   _Float16* xbuf = reinterpret_cast<_Float16*>(static_cast<char*>(ws) + 256);

@@ -17,15 +17,17 @@ def shard_range(n_total, rank, world):
     return lo, lo + base + (1 if rank < extra else 0)
 
 
-def gather_logits(local, n_total=None, out=None):
+def gather_logits(local, n_total=None, out=None, force_collective=False):
     """All-gather per-shard [n_r, K] tensors into the full [n, K] in rank order.
 
     With ``n_total`` the shard sizes follow ``shard_range`` and need no exchange (the per-step path
     of bench.py); without it they are all-gathered first.  Equal shards use one
     ``all_gather_into_tensor`` (into ``out`` when given, e.g. a buffer reused across steps); ragged
-    shards pad to the largest and trim."""
+    shards pad to the largest and trim.  A one-rank group returns ``local`` (copied into ``out``)
+    without a collective unless ``force_collective``: the GPU test runs the RCCL calls of the
+    multi-rank path at world size 1 with it (tests/test_gpu_rccl.py)."""
     world = dist.get_world_size() if dist.is_initialized() else 1
-    if world == 1:
+    if world == 1 and not (force_collective and dist.is_initialized()):
         if out is not None:
             out.copy_(local)
             return out

@@ -112,19 +112,24 @@ def load_model(path, kind=None, n_classes=None, head=None, seed=0, device=None,
     lay = _layout_from_path(path)
     kind = (lay[0] if lay else _kind_from_path(path)) if kind is None else kind
     synthetic = False
-    try:
+    shard = os.path.join(path, 'variables', 'variables.data-00000-of-00001')
+    if os.path.exists(shard):
+        # present: any failure (a corrupt bundle, libmmla.so missing for the CRC) is a real error
         W, (bkind, bk, bhead) = tfbundle.load_bundle(path, with_layout=True)
         if bkind != kind:
             raise ValueError(f'{path}: bundle holds a {"OD" if bkind == weights.OD else "SI"} model')
         if kind == weights.SI:
             n_classes = bk
             head = bhead if head is None else head
-    except (FileNotFoundError, OSError) as e:
+    else:
         if not allow_synthetic:
             raise FileNotFoundError(
-                f'{path}: trained variables not found ({e}); the reference ships only '
+                f'{path}: trained variables not found ({shard} is absent); the reference ships only '
                 f'variables.index (.MISSING_LARGE_BLOBS). Pass allow_synthetic=True for seeded '
-                f'synthetic weights in the reference layout.') from e
+                f'synthetic weights in the reference layout.')
+        if lay is not None and kind == weights.SI:   # the layout the index names (K, head)
+            n_classes = lay[1] if n_classes is None else n_classes
+            head = lay[2] if head is None else head
         warnings.warn(f'{path}: trained weights absent (reference .MISSING_LARGE_BLOBS); using seeded '
                       f'synthetic weights in the reference layout (seed={seed})')
         W = weights.synthetic(kind, seed=seed, n_classes=n_classes)

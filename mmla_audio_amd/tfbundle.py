@@ -183,7 +183,11 @@ def layout(shapes):
         if kind == weights.OD:
             items, n_classes, head = weights.od_spec(), 2, _lib.HEAD_SOFTMAX
         else:
-            n_classes = shapes['layer_with_weights-42/kernel'][1]
+            head_kernel = shapes.get('layer_with_weights-42/kernel')
+            if head_kernel is None or len(head_kernel) != 2:
+                raise ValueError('unrecognised bundle layout: an SI base model without its Dense '
+                                 'head (layer_with_weights-42/kernel)')
+            n_classes = head_kernel[1]
             items = weights.si_spec(n_classes)
             head = _lib.HEAD_SOFTMAX
         mapping = {k: k for k in top}
@@ -192,6 +196,9 @@ def layout(shapes):
             raise ValueError('unrecognised bundle layout: neither a base model nor a '
                              'transfer_learning (nested base + customized_dense) model')
         kind = weights.SI
+        if len(shapes['layer_with_weights-1/kernel']) != 2:
+            raise ValueError('unrecognised bundle layout: layer_with_weights-1/kernel is not a '
+                             'Dense kernel')
         n_classes = shapes['layer_with_weights-1/kernel'][1]
         head = _lib.HEAD_SIGMOID
         items = weights.si_spec(n_classes)

@@ -155,6 +155,12 @@ def test_float_pcm_outside_split_range():
     with pytest.raises(_lib.MmlaError) as e:
         c.od_features(bad[None])
     assert e.value.code == _lib.MMLA_E_RANGE
+    assert 'clip 0 sample 1234' in str(e.value)
+    # the kernel's range word flags the host call; the host re-scan names the clip of a batch
+    with pytest.raises(_lib.MmlaError) as e:
+        c.od_features(np.stack([loud, loud, bad]))
+    assert e.value.code == _lib.MMLA_E_RANGE and 'clip 2 sample 1234' in str(e.value)
+    assert np.isfinite(c.od_features(np.stack([loud, loud]))['db']).all()   # the word was reset
     nan = loud.copy()
     nan[10] = np.nan
     with pytest.raises(_lib.MmlaError):
