@@ -140,6 +140,9 @@ struct mmla_ctx {
   // OD blocks 4-9 as one fused kernel each (odu.hip: t1 on chip); env MMLA_NO_ODU=1 at create: the
   // conv_h3 pairs (A/B, bit-identical)
   bool odu = true;
+  // OD blocks 1-3 as rolling column strips (rbs.hip); env MMLA_RB_TILE=1 at create: the 16 x 16 tile
+  // kernels of resblk.hip instead
+  bool rbs = true;
   // batches of <= lstm_split_max clips: the 3xFP16 BiLSTM with each direction's hidden units on eight workgroups
   // (nets.hip bilstm_h3_split_kernel); env MMLA_NO_LSTM_SPLIT=1 at create: one workgroup per direction
   bool lstm_split = true;
@@ -864,9 +867,18 @@ int run_od_net(mmla_ctx* c, const uint8_t* img_u8, const float* img_f32, int64_t
   float* T2 = static_cast<float*>(pt2);
   // Conv2D(16, 1x1) on the PNG image (overlap_detector_temp.py:282): computed inside block 1's
   // staging when block 1 runs fused (resblk.hip STEM), else its own launch
-  const bool fuse_stem = c->precision == MMLA_PREC_F16X3 && stop != 0 && W.blk[0].c3.fh &&
-                         W.blk[0].c4.fh && W.blk[0].sc.fh &&
-                         resblk_supported(W.blk[0].c3.cin, W.blk[0].c3.cout, POOL[0]);
+  // blocks 1-3 as rolling strips (rbs.hip) on the conv_h3 weight layout
+  auto rbs_ok = [&](int b, int hh, int ww) {
+    const OdBlock& B = W.blk[b];
+    return c->rbs && c->precision == MMLA_PREC_F16X3 && B.c3.wh && B.c4.wh && (!POOL[b] || B.sc.wh) &&
+           B.c3.cin_pad == B.c3.cin && B.c3.cout_pad == 32 && B.c4.cin_pad == 32 && B.c4.cout_pad == 32 &&
+           B.c4.kh == 4 && B.c4.kw == 1 && (!POOL[b] || (B.sc.cin_pad == B.c3.cin && B.sc.cout_pad == 32)) &&
+           rbs_supported(hh, ww, B.c3.cin, B.c3.cout, POOL[b]);
+  };
+  const bool rbs_stem = stop != 0 && rbs_ok(0, OD_H, OD_W);
+  const bool fuse_stem = c->precision == MMLA_PREC_F16X3 && stop != 0 &&
+                         (rbs_stem || (W.blk[0].c3.fh && W.blk[0].c4.fh && W.blk[0].sc.fh &&
+                                       resblk_supported(W.blk[0].c3.cin, W.blk[0].c3.cout, POOL[0])));
   if (!fuse_stem)
     LAUNCH(c, MMLA_STAGE_GLUE, 2.0 * n * OD_PIX * 3 * 16,
            od_stem_launch(img_u8, img_f32, n * OD_PIX, W.stem.cout_pad, W.stem.wt, W.stem.bias, X,
@@ -879,6 +891,58 @@ int run_od_net(mmla_ctx* c, const uint8_t* img_u8, const float* img_f32, int64_t
   }
   for (int b = 0; b < 9; ++b) {   // res_block, overlap_detector_temp.py:253-277
     const OdBlock& B = W.blk[b];
+    if ((b == 0 ? rbs_stem && fuse_stem : rbs_ok(b, h, w))) {
+      // whole block in one launch, rolling down 16-column strips: t1 stays in LDS (rbs.hip)
+      ResBlkArgs r{};
+      r.x = X;
+      r.w1h = B.c3.wh;
+      r.w1l = B.c3.wl;
+      r.b1 = B.c3.bias;
+      r.u1 = B.c3.unscale();
+      r.u2 = B.c4.unscale();
+      r.us = POOL[b] ? B.sc.unscale() : 0.0f;
+      r.s1 = B.bn_in.scale;
+      r.t1 = B.bn_in.shift;
+      r.w2h = B.c4.wh;
+      r.w2l = B.c4.wl;
+      r.b2 = B.c4.bias;
+      r.s2 = B.bn_mid.scale;
+      r.t2 = B.bn_mid.shift;
+      if (POOL[b]) {
+        r.wsh = B.sc.wh;
+        r.wsl = B.sc.wl;
+        r.bs = B.sc.bias;
+      }
+      r.y = T1;
+      if (b == 0) {
+        r.x = nullptr;
+        r.img8 = img_u8;
+        r.imgf = img_u8 ? nullptr : img_f32;
+        r.wst = W.stem.wt;
+        r.bst = W.stem.bias;
+        r.ldst = W.stem.cout_pad;
+      }
+      r.n = (int)n;
+      r.h = h;
+      r.w = w;
+      r.range_flag = c->range_ptr;
+      LAUNCH(c, MMLA_STAGE_CONV,
+             (b == 0 ? 2.0 * n * h * w * 3 * 16 : 0.0) +
+             2.0 * n * h * w * (9.0 * B.c3.cin * B.c3.cout + 4.0 * B.c4.cin * B.c4.cout) +
+                 (POOL[b] ? 2.0 * n * ((h + 1) / 2) * ((w + 1) / 2) * B.sc.cin * B.sc.cout : 0.0),
+             rbs_launch(r, B.c3.cin, B.c3.cout, POOL[b], c->stream));
+      if (POOL[b]) {
+        h = (h + 1) / 2;
+        w = (w + 1) / 2;
+      }
+      std::swap(X, T1);
+      if (stop == b + 1) {
+        *tap = X;
+        *tap_n = n * h * w * CH[b];
+        return MMLA_OK;
+      }
+      continue;
+    }
     if (c->precision == MMLA_PREC_F16X3 && B.c3.fh && B.c4.fh && B.c4.kpad == 4 * B.c4.cin &&
         (!POOL[b] || B.sc.fh) &&
         resblk_supported(B.c3.cin, B.c3.cout, POOL[b])) {
@@ -1319,6 +1383,7 @@ int mmla_create(int device, mmla_ctx** out) {
   if (const char* sp = std::getenv("MMLA_DEBUG_LSTM_SPIN")) c->lstm_spin = std::atoi(sp);
   if (const char* sd = std::getenv("MMLA_NO_SIPAD")) c->si_pad_feat = std::atoi(sd) == 0;
   if (const char* ou = std::getenv("MMLA_NO_ODU")) c->odu = std::atoi(ou) == 0;
+  if (const char* rt = std::getenv("MMLA_RB_TILE")) c->rbs = std::atoi(rt) == 0;
   // a BLOCKING stream: it orders with the legacy default (NULL) stream, on which PyTorch's default
   // stream enqueues -- so a device-pointer call sees tensors a torch kernel or copy just produced
   // without an explicit synchronisation (a non-blocking stream raced them: a 65 536-clip call read

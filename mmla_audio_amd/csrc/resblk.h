@@ -41,3 +41,9 @@ hipError_t resblk_launch(ResBlkArgs a, int cin, int c, bool pool, hipStream_t st
 // (GEMM 1's 3x3 and GEMM 2's conv(4,1) weights; the 1x1 shortcut keeps the [cout][kpad] rows).
 void resblk_split_weights(const float* w, int taps, int cin, int cout, int kpad, uint16_t* hi,
                           uint16_t* lo, bool frag, float wscale);
+
+// Blocks 1-3 as rolling 16-column strips on 32x32x16 MFMAs (rbs.hip).  The weights are in the
+// conv_h3 layout (conv_h3_split_weights: w1h / w1l the 3x3, w2h / w2l the (4,1), wsh / wsl the 1x1
+// shortcut); a.h / a.w are the block's input size.  Block 1 (pool) needs the stem fused (img8 / imgf).
+bool rbs_supported(int h, int w, int cin, int c, bool pool);
+hipError_t rbs_launch(const ResBlkArgs& a, int cin, int c, bool pool, hipStream_t stream);
