@@ -49,7 +49,6 @@ constexpr int R = 8;               // output rows per chunk (4 waves x 2 rows)
 constexpr int C = 32;              // output channels of blocks 1-3
 constexpr float L2E_16 = 1.4426950408889634f / 16.0f;   // log2(e) / 2^4
 constexpr float SPLIT_MAX = 65504.0f;                    // largest finite fp16
-constexpr int PF = 3;              // weight fragments in flight (k-steps)
 #ifndef RBS_TRACE
 #define RBS_TRACE 0
 #endif
@@ -71,6 +70,15 @@ __device__ unsigned long long rbs_trace_buf[2048 * 4 * 4 * 8];
 #endif
 #ifndef RBS_W2L23
 #define RBS_W2L23 0
+#endif
+#ifndef RBS_PF1
+#define RBS_PF1 3
+#endif
+#ifndef RBS_PF23
+#define RBS_PF23 3
+#endif
+#ifndef RBS_W1L1
+#define RBS_W1L1 0
 #endif
 #ifndef RBS_MB1
 #define RBS_MB1 3
@@ -129,6 +137,8 @@ struct SG {
   static constexpr int KS1 = 9 * KPT, KS2 = 8;
   static constexpr bool W2L = CIN == 16 ? RBS_W2L1 : RBS_W2L23;   // GEMM 2's weights in LDS
   static constexpr int MINB = CIN == 16 ? RBS_MB1 : RBS_MB23;      // resident workgroups per CU
+  static constexpr int PF = CIN == 16 ? RBS_PF1 : RBS_PF23;        // GEMM 1 weight k-steps in flight
+  static constexpr bool W1L = CIN == 16 && RBS_W1L1;               // GEMM 1's weights in LDS
   static constexpr int PD = CIN == 16 ? 1 : 2;                      // input prefetch distance (chunks)
   static_assert(H % R == 0, "geometry");
   static_assert(NT % QPP == 0, "a thread's channel quad is fixed");
@@ -161,6 +171,7 @@ __global__ void __launch_bounds__(NT, (SG<H, W, CIN, POOL>::MINB)) rbs_kernel(Re
   __shared__ float4 spar[3 * C / 4 + (STEM ? 16 : 0)];
   // GEMM 2's weights in fragment order (W2L): [k-step][lane][8] hi, then lo
   __shared__ __attribute__((aligned(16))) _Float16 sw2[G::W2L ? 2 * G::KS2 * 512 : 8];
+  __shared__ __attribute__((aligned(16))) _Float16 sw1[G::W1L ? 2 * G::KS1 * 512 : 8];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -190,6 +201,12 @@ __global__ void __launch_bounds__(NT, (SG<H, W, CIN, POOL>::MINB)) rbs_kernel(Re
   // in issue order: a weight load behind them would wait for HBM)
   const __amdgpu_buffer_rsrc_t rw1h = rbs_rsrc(a.w1h), rw1l = rbs_rsrc(a.w1l);
   f16x8 w2h[G::W2L ? 1 : G::KS2], w2l[G::W2L ? 1 : G::KS2];
+  if constexpr (G::W1L) {
+    for (int e = tid; e < 2 * G::KS1 * 64; e += NT) {   // 16-B pieces
+      const int pl = e / (G::KS1 * 64), i = e - pl * (G::KS1 * 64);
+      *reinterpret_cast<f16x8*>(sw1 + 8 * e) = *reinterpret_cast<const f16x8*>((pl ? a.w1l : a.w1h) + 8 * i);
+    }
+  }
   if constexpr (G::W2L) {
     for (int e = tid; e < 2 * G::KS2 * 64; e += NT) {   // 16-B pieces
       const int pl = e / (G::KS2 * 64), i = e - pl * (G::KS2 * 64);
@@ -329,12 +346,14 @@ __global__ void __launch_bounds__(NT, (SG<H, W, CIN, POOL>::MINB)) rbs_kernel(Re
 #pragma unroll
     for (int ks = 0; ks < G::KPT; ++ks) xco[dx][ks] = xoff<CIN>(0, nc + dx, G::KPT == 2 ? 2 * ks + h : h);
 
-  f16x8 w1h[PF], w1l[PF];   // GEMM 1's weight ring (PF k-steps ahead), first steps issued early
+  f16x8 w1h[G::W1L ? 1 : G::PF], w1l[G::W1L ? 1 : G::PF];   // GEMM 1's weight ring (PF k-steps ahead), first steps issued early
   auto gemm1_issue = [&]() {
+    if constexpr (!G::W1L) {
 #pragma unroll
-    for (int s = 0; s < PF; ++s) {
-      w1h[s] = rbs_frag(rw1h, s * 512, lofs);
-      w1l[s] = rbs_frag(rw1l, s * 512, lofs);
+      for (int s = 0; s < G::PF; ++s) {
+        w1h[s] = rbs_frag(rw1h, s * 512, lofs);
+        w1l[s] = rbs_frag(rw1l, s * 512, lofs);
+      }
     }
   };
   auto gemm1 = [&](int j0) -> f32x16 {
@@ -352,12 +371,28 @@ __global__ void __launch_bounds__(NT, (SG<H, W, CIN, POOL>::MINB)) rbs_kernel(Re
     };
     f16x8 nxh = *reinterpret_cast<const f16x8*>(sx + xo(0));
     f16x8 nxl = *reinterpret_cast<const f16x8*>(sx + G::XPLANE + xo(0));
+    f16x8 nbh, nbl;
+    if constexpr (G::W1L) {
+      nbh = *reinterpret_cast<const f16x8*>(sw1 + lofs);
+      nbl = *reinterpret_cast<const f16x8*>(sw1 + G::KS1 * 512 + lofs);
+    }
 #pragma unroll
     for (int s = 0; s < G::KS1; ++s) {
-      const f16x8 bh = w1h[s % PF], bl = w1l[s % PF];
-      if (s + PF < G::KS1) {
-        w1h[s % PF] = rbs_frag(rw1h, (s + PF) * 512, lofs);
-        w1l[s % PF] = rbs_frag(rw1l, (s + PF) * 512, lofs);
+      f16x8 bh, bl;
+      if constexpr (G::W1L) {
+        bh = nbh;
+        bl = nbl;
+        if (s + 1 < G::KS1) {
+          nbh = *reinterpret_cast<const f16x8*>(sw1 + (s + 1) * 512 + lofs);
+          nbl = *reinterpret_cast<const f16x8*>(sw1 + (G::KS1 + s + 1) * 512 + lofs);
+        }
+      } else {
+        bh = w1h[s % G::PF];
+        bl = w1l[s % G::PF];
+        if (s + G::PF < G::KS1) {
+          w1h[s % G::PF] = rbs_frag(rw1h, (s + G::PF) * 512, lofs);
+          w1l[s % G::PF] = rbs_frag(rw1l, (s + G::PF) * 512, lofs);
+        }
       }
       const f16x8 xh = nxh, xl = nxl;
       if (s + 1 < G::KS1) {
