@@ -12,14 +12,13 @@
 // matrix stages on the f16 MFMA in error-compensated 3xFP16 (the v3 kernel below; the earlier
 // VALU-FFT kernels and their measurements are in DESIGN.md section 4).
 //
-// Built WITHOUT packed-FP32 instructions (v_pk_fma/mul/add_f32; Makefile NO_PK_F32): on MI355X a
-// front-end wave using them returned wrong values in one 16-lane quarter of an instruction, a few
-// times per thousand waves, while MFMA workgroups of another stream (resblk.hip) shared the CUs;
-// without them the same co-run is bit-exact and the kernel is 7-12 % faster.
-// (A per-kernel target attribute is not enough: the HIP headers' helpers, e.g. float2's constructor
-// and threadIdx, then stop inlining across the feature mismatch and spill to scratch.)
-// (Round 5: the MFMA kernel below assembles identically with and without the flag -- it emits no
-// packed-FP32 instruction either way; the flag guards future edits.)
+// Built with the packed-FP32 target feature off (Makefile NO_PK_F32).  Today that is a no-op guard:
+// the kernel below assembles to the same instructions with and without it (it emits no v_pk_*_f32).
+// History: the deleted v2 VALU-FFT front-end, which did use half-swapped packed FMAs, returned wrong
+// values in one 16-lane quarter of an instruction a few times per thousand waves while MFMA workgroups
+// of another stream shared its CUs; built without packed FP32 the same co-run was bit-exact.  The
+// hardware-side root cause was never isolated (co-run section); tests/test_gpu_corun.py
+// stays the runtime guard.
 //
 // Accumulation is float32 (the reference runs the FFT in float64 and stores complex64; the measured
 // deviation on the normalised log-mel is ~1e-5, tolerance 1e-4).  The scalar steps
@@ -71,12 +70,6 @@ typedef uint16_t us2 __attribute__((ext_vector_type(2)));
 
 constexpr int NWV = 16;                       // waves per workgroup (one workgroup per CU)
 constexpr int NTH = 64 * NWV;
-// FE_INPLACE (dev variant): the mel writes log2 S into the clip's own norm slot instead
-// of keeping it in 20 registers per lane; the epilogue re-reads it and rescales in place.  Only the
-// norm-output instantiations change (the pipeline's image-only launch has no norm buffer).
-#ifndef FE_INPLACE
-#define FE_INPLACE 0
-#endif
 constexpr int TF = 32;                        // frames per tile = the MFMA's 32 columns
 constexpr int NTILE = (NF + TF - 1) / TF;     // 5 (frames 151..159 are computed and dropped)
 constexpr int TQ = 344;                       // q columns of T: p = 16 q + n1; q < 335 staged per tile,
@@ -561,8 +554,7 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
   // ---- mel of tile t on the f32 MFMA: S[16 bands][16 frames] = A (16 x 4 k-steps) . P (bins x frames),
   //      exact float32 products and sums (the reference's np.dot is float32); K-steps in batches of 4
   //      whose 8 LDS reads are issued before their MFMAs; A columns past a band's support are zero ----
-  constexpr bool INPL = FE_INPLACE && NM;
-  auto mel = [&](auto T_, const float* P, int64_t mclip) {
+  auto mel = [&](auto T_, const float* P) {
     constexpr int t = decltype(T_)::value;
     int l = lane;
     asm volatile("" : "+v"(l));
@@ -590,14 +582,7 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
     const bool live = TF * t + TF <= NF || TF * t + 16 * m_fh + (l & 15) < NF;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      if constexpr (INPL) {   // log2 S to the norm slot (the epilogue's offsets)
-        const auto rn = wave_rsrc(a.norm + mclip * (NMEL * NF), NMEL * NF * 4);
-        const uint32_t vf = (uint32_t)(4 * (l >> 4) * NF + (l & 15)) * 4u;
-        const int so = (16 * m_bt * NF + 16 * m_fh) * 4 + (i * NF + TF * t) * 4;
-        if (live) __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, lg2m(acc[i])), rn, vf, so, 0);
-      } else {
-        dbv[t][i] = lg2m(acc[i]);
-      }
+      dbv[t][i] = lg2m(acc[i]);
       if (live) {
         smax = fmaxf(smax, acc[i]);
         smin = fminf(smin, acc[i]);
@@ -647,7 +632,6 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
     // image row 127 - (16 bt + 4 (l >> 4) + i) = (112 - 16 bt) + (12 - 4 (l >> 4)) + (3 - i)
     const uint32_t vi = (uint32_t)((12 - 4 * (l >> 4)) * NF + (l & 15)) * 3u;
     const int si = ((112 - 16 * m_bt) * NF + 16 * m_fh) * 3;
-    if constexpr (INPL) wave_stores_done();   // this lane's log2 S stores are visible to its reloads
 #pragma unroll
     for (int t = 0; t < NTILE; ++t) {
       if (TF * t + TF > NF && TF * t + fr >= NF) continue;
@@ -655,13 +639,7 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
       if (IMG) rr = (uint32_t)(int)(((double)sm.zc[par][TF * t + fr] / 400.0) * 255.0) & 255u;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        float lg;
-        if constexpr (INPL) {
-          lg = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rn, vf, sf + (i * NF + TF * t) * 4, 0));
-        } else {
-          lg = dbv[t][i];
-        }
-        const float d = fmaxf(fmaf(lg, DB_PER_LOG2, nref), thr);
+        const float d = fmaxf(fmaf(dbv[t][i], DB_PER_LOG2, nref), thr);
         // (d - min) / (max - min) as a multiply by the reciprocal (<= 2 ulp); 0 * inf =
         // NaN keeps the digital-silence NaN.  The (i, t) part of the offset is wave-uniform: it
         // rides in soffset (a scalar add), the lane's part is the one VGPR vf
@@ -712,9 +690,9 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
       // (it runs in B on every wave: the youngest waves of each SIMD in A measured 0.2964 vs 0.2941 ms)
       auto mel_prev = [&]() {
         if constexpr (t > 0) {
-          mel(tile_c<t - 1>{}, p_r, clip);
+          mel(tile_c<t - 1>{}, p_r);
         } else if (ci > 0) {
-          mel(tile_c<NTILE - 1>{}, p_r, clip - gridDim.x);
+          mel(tile_c<NTILE - 1>{}, p_r);
         }
       };
       // ---- interval A ----

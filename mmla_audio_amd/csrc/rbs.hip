@@ -99,11 +99,13 @@ MMLA_DEV f16x8 rbs_frag(__amdgpu_buffer_rsrc_t r, int u, int lofs) {
   return __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(r, (uint32_t)lofs * 2u, u * 2, 0));
 }
 
-// 16 ELU(u) from u16 = 16 u: u16 > 0 ? u16 : 16 exp(u) - 16 (TF Elu: exp(x) - 1 for x < 0; the power-of-
-// two scaling commutes with every rounding, so this equals 16 * (exp(u) - 1) bit for bit)
+// 16 ELU(u) from u16 = 16 u (TF Elu: exp(x) - 1 for x < 0; the power-of-two scaling commutes with every
+// rounding).  With e = 16 exp(u) - 16: u > 0 gives 0 < u < e (or e = inf), u <= 0 gives u <= e <= 0,
+// so ELU is the median of (u, e, 0) -- one v_med3 instead of a compare and a select.  (Where the
+// rounding of e puts it a hair below u, for |u16| ~ 1e-3, the median returns u: within 1e-6.)
 MMLA_DEV float elu16(float u16) {
-  const float e = __builtin_amdgcn_exp2f(u16 * L2E_16);
-  return u16 > 0.0f ? u16 : fmaf(e, 16.0f, -16.0f);
+  const float e = fmaf(__builtin_amdgcn_exp2f(u16 * L2E_16), 16.0f, -16.0f);
+  return __builtin_amdgcn_fmed3f(u16, e, 0.0f);
 }
 
 // v' (already x 2^4) = hi + lo, both fp16 (RNE); lo = f16(v' - hi) exactly rounded once (v_fma_mix)
@@ -180,7 +182,7 @@ __global__ void __launch_bounds__(NT, (SG<H, W, CIN, POOL>::MINB)) rbs_kernel(Re
   const int clip = (int)(bid / G::STRIPS);
   const int w0 = (int)(bid - (uint32_t)clip * G::STRIPS) * TW;
   const int lofs = lane * 8;
-  bool rbad = false;
+  float rmax = 0.0f;   // 3xFP16 range guard: the largest |operand| this thread split (ResBlkArgs::range_flag)
 
   // ---- parameters -------------------------------------------------------------------------------
   float* const sp = reinterpret_cast<float*>(spar);
@@ -304,7 +306,10 @@ __global__ void __launch_bounds__(NT, (SG<H, W, CIN, POOL>::MINB)) rbs_kernel(Re
     return load_src(r0 + (int)((ti >> 14) & 15), task_col(j), (ti >> 18) & 1);
   };
   // BN1 + ELU (+ the stem) + split of one task's 4 channels at x row ih, into the x ring at lds
-  auto stage4 = [&](int ih, int lds, bool in, float4 v) {
+  // BN1 + ELU (+ the stem) + split of one task's 4 channels into the x ring at half offset o; MASK:
+  // zero unless `in` (the 3x3 conv's padding rows; padding columns are zeroed once, see below)
+  auto stage4 = [&](int o, bool in, float4 v, auto MASK_) {
+    constexpr bool MASK = decltype(MASK_)::value;
     if constexpr (STEM) v = img_px(v);
     float u[4];
 #pragma unroll
@@ -320,22 +325,32 @@ __global__ void __launch_bounds__(NT, (SG<H, W, CIN, POOL>::MINB)) rbs_kernel(Re
     }
     float e[4];
 #pragma unroll
-    for (int c = 0; c < 4; ++c) e[c] = in ? elu16(u[c]) : 0.0f;   // zero: the 3x3 conv's padding
-    rbad |= !(amax4(e[0], e[1], e[2], e[3]) < SPLIT_MAX);
+    for (int c = 0; c < 4; ++c) e[c] = (!MASK || in) ? elu16(u[c]) : 0.0f;
+    rmax = fmaxf(rmax, amax4(e[0], e[1], e[2], e[3]));
     f16x4 hv, lv;
     split4(e[0], e[1], e[2], e[3], hv, lv);
-    const int o = ((ih + 1) % G::XRING) * G::XROW + lds;
     *reinterpret_cast<f16x4*>(sx + o) = hv;
     *reinterpret_cast<f16x4*>(sx + G::XPLANE + o) = lv;
   };
-  auto stage_task = [&](int r0, int j, float4 v) {
+  // a chunk's task j: rows r0 .. r0 + 7; tasks on a column outside the image do nothing (their ring
+  // column stays zero); rows past the image only occur in the last chunk (MASK)
+  auto stage_task = [&](int r0, int j, float4 v, auto MASK_) {
     const uint32_t ti = tinfo[j];
-    if (!((ti >> 19) & 1)) return;
-    const int ih = r0 + (int)((ti >> 14) & 15);
-    const bool in = ((ti >> 18) & 1) && ih >= 0 && ih < H;
-    stage4(ih, (int)(ti & 16383), in, v);
+    if ((ti >> 18) != 3u) return;   // task exists and its column is inside the image
+    const int rr = (int)((ti >> 14) & 15);
+    uint32_t slot = (uint32_t)((r0 + 1) % G::XRING) + (uint32_t)rr;   // (r0 + 1) % XRING: scalar
+    slot = min(slot, slot - (uint32_t)G::XRING);
+    stage4((int)slot * G::XROW + (int)(ti & 16383), r0 + rr < H, v, MASK_);
   };
-
+  // the ring's columns outside the image (strip 0: image column -1; the last strip: columns >= W),
+  // zeroed once in every slot and both planes: no task writes them
+  for (int e = tid; e < 2 * G::XRING * G::XW * G::QPP; e += NT) {
+    const int pl = e / (G::XRING * G::XW * G::QPP), r = e - pl * (G::XRING * G::XW * G::QPP);
+    const int slot = r / (G::XW * G::QPP), x = (r / G::QPP) % G::XW, qq = r % G::QPP;
+    const int iw = w0 - 1 + x;
+    if (iw < 0 || iw >= W)
+      *reinterpret_cast<f16x4*>(sx + pl * G::XPLANE + xoff<CIN>(slot, x, qq >> 1) + 4 * (qq & 1)) = f16x4{};
+  }
   // ---- GEMM 1 for t1 rows j0, j0 + 1 (one 32-pixel tile, natural order: pixel n = lane & 31 is row
   //      j0 + (n >> 4), column n & 15) as t1^T: acc[4 jj + i] = channel 8 jj + 4 h + i of pixel n ----
   const int n = lane & 31, nr = n >> 4, nc = n & 15;
@@ -421,7 +436,7 @@ __global__ void __launch_bounds__(NT, (SG<H, W, CIN, POOL>::MINB)) rbs_kernel(Re
         e[1] = elu16(fmaf(acc[4 * jj + 1], sv.y, cv.y));
         e[2] = elu16(fmaf(acc[4 * jj + 2], sv.z, cv.z));
         e[3] = elu16(fmaf(acc[4 * jj + 3], sv.w, cv.w));
-        rbad |= !(amax4(e[0], e[1], e[2], e[3]) < SPLIT_MAX);
+        rmax = fmaxf(rmax, amax4(e[0], e[1], e[2], e[3]));
         f16x4 hv, lv;
         split4(e[0], e[1], e[2], e[3], hv, lv);
         const int o = toff<POOL>(slot, j, nc, jj) + 4 * h;
@@ -449,7 +464,8 @@ __global__ void __launch_bounds__(NT, (SG<H, W, CIN, POOL>::MINB)) rbs_kernel(Re
       const int ih = rr - 1, iw = w0 - 1 + x;
       const bool col_ok = iw >= 0 && iw < W;
       const float4 v = load_src(ih, iw, col_ok);
-      if (t < T0) stage4(ih, xoff<CIN>(0, x, q >> 1) + 4 * (q & 1), col_ok && ih >= 0, v);
+      if (t < T0 && col_ok)
+        stage4(xoff<CIN>((ih + 1) % G::XRING, x, q >> 1) + 4 * (q & 1), ih >= 0, v, std::true_type{});
     }
     for (int e = tid; e < 2 * G::TROW / 8; e += NT)   // t1 row -1 (slot 0), both planes
       *reinterpret_cast<f16x8*>(st + (e >= G::TROW / 8 ? G::TPLANE - G::TROW : 0) + 8 * e) = f16x8{};
@@ -486,8 +502,13 @@ __global__ void __launch_bounds__(NT, (SG<H, W, CIN, POOL>::MINB)) rbs_kernel(Re
     const int j0 = R * k + 2 + 2 * wave;  // this wave's t1 rows (GEMM 1)
     const int o0 = R * k + 2 * wave;      // this wave's output rows (GEMM 2)
     // ---- stage the new x rows, start GEMM 1's weight stream ------------------------------------
+    if (k + 1 < G::NCHUNK) {
 #pragma unroll
-    for (int j = 0; j < G::MAXT; ++j) stage_task(rx0, j, pre[j]);
+      for (int j = 0; j < G::MAXT; ++j) stage_task(rx0, j, pre[j], std::false_type{});
+    } else {
+#pragma unroll
+      for (int j = 0; j < G::MAXT; ++j) stage_task(rx0, j, pre[j], std::true_type{});
+    }
     gemm1_issue();
     RBS_T(1);
     __syncthreads();
@@ -600,7 +621,7 @@ __global__ void __launch_bounds__(NT, (SG<H, W, CIN, POOL>::MINB)) rbs_kernel(Re
           s = fmaf(px.z, wv.z, s);
           o8[c] = sc_col < W ? 16.0f * (s + wv.w) : 0.0f;
         }
-        rbad |= !(fmaxf(amax4(o8[0], o8[1], o8[2], o8[3]), amax4(o8[4], o8[5], o8[6], o8[7])) < SPLIT_MAX);
+        rmax = fmaxf(rmax, fmaxf(amax4(o8[0], o8[1], o8[2], o8[3]), amax4(o8[4], o8[5], o8[6], o8[7])));
         f16x4 h0, l0, h1, l1;
         split4(o8[0], o8[1], o8[2], o8[3], h0, l0);
         split4(o8[4], o8[5], o8[6], o8[7], h1, l1);
@@ -644,7 +665,7 @@ __global__ void __launch_bounds__(NT, (SG<H, W, CIN, POOL>::MINB)) rbs_kernel(Re
 #pragma unroll 1
     for (int k = 0; k < G::NCHUNK; ++k) chunk(k, preA);
   }
-  if (rbad && a.range_flag) *a.range_flag = 1;
+  if (!(rmax < SPLIT_MAX) && a.range_flag) *a.range_flag = 1;
 }
 
 template <int H, int W, int CIN, bool POOL, bool STEM>
