@@ -62,30 +62,6 @@ __device__ unsigned long long rbs_trace_buf[2048 * 4 * 4 * 8];
 #define RBS_T(i) do { } while (0)
 #define RBS_TFLUSH() do { } while (0)
 #endif
-#ifndef RBS_SB
-#define RBS_SB 1
-#endif
-#ifndef RBS_W2L1
-#define RBS_W2L1 1
-#endif
-#ifndef RBS_W2L23
-#define RBS_W2L23 0
-#endif
-#ifndef RBS_PF1
-#define RBS_PF1 3
-#endif
-#ifndef RBS_PF23
-#define RBS_PF23 3
-#endif
-#ifndef RBS_W1L1
-#define RBS_W1L1 0
-#endif
-#ifndef RBS_MB1
-#define RBS_MB1 3
-#endif
-#ifndef RBS_MB23
-#define RBS_MB23 2
-#endif
 
 MMLA_DEV __amdgpu_buffer_rsrc_t rbs_rsrc(const void* p) {
   const uint64_t u = reinterpret_cast<uint64_t>(p);
@@ -137,10 +113,11 @@ struct SG {
   static constexpr int MAXT0 = (4 * XW * QPP + NT - 1) / NT;     // the prologue's 4 rows
   static constexpr int KPT = CIN / 16;                  // 16-deep k-steps per tap
   static constexpr int KS1 = 9 * KPT, KS2 = 8;
-  static constexpr bool W2L = CIN == 16 ? RBS_W2L1 : RBS_W2L23;   // GEMM 2's weights in LDS
-  static constexpr int MINB = CIN == 16 ? RBS_MB1 : RBS_MB23;      // resident workgroups per CU
-  static constexpr int PF = CIN == 16 ? RBS_PF1 : RBS_PF23;        // GEMM 1 weight k-steps in flight
-  static constexpr bool W1L = CIN == 16 && RBS_W1L1;               // GEMM 1's weights in LDS
+  // block 1 keeps GEMM 2's weights in LDS to fit 3 workgroups per CU; blocks 2-3 keep them in
+  // registers at 2 (measured: deeper weight prefetch or LDS-resident GEMM 1 weights do not pay)
+  static constexpr bool W2L = CIN == 16;                // GEMM 2's weights in LDS
+  static constexpr int MINB = CIN == 16 ? 3 : 2;        // resident workgroups per CU
+  static constexpr int PF = 3;                          // GEMM 1 weight k-steps in flight
   static constexpr int PD = CIN == 16 ? 1 : 2;                      // input prefetch distance (chunks)
   static_assert(H % R == 0, "geometry");
   static_assert(NT % QPP == 0, "a thread's channel quad is fixed");
@@ -173,7 +150,6 @@ __global__ void __launch_bounds__(NT, (SG<H, W, CIN, POOL>::MINB)) rbs_kernel(Re
   __shared__ float4 spar[3 * C / 4 + (STEM ? 16 : 0)];
   // GEMM 2's weights in fragment order (W2L): [k-step][lane][8] hi, then lo
   __shared__ __attribute__((aligned(16))) _Float16 sw2[G::W2L ? 2 * G::KS2 * 512 : 8];
-  __shared__ __attribute__((aligned(16))) _Float16 sw1[G::W1L ? 2 * G::KS1 * 512 : 8];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -203,12 +179,6 @@ __global__ void __launch_bounds__(NT, (SG<H, W, CIN, POOL>::MINB)) rbs_kernel(Re
   // in issue order: a weight load behind them would wait for HBM)
   const __amdgpu_buffer_rsrc_t rw1h = rbs_rsrc(a.w1h), rw1l = rbs_rsrc(a.w1l);
   f16x8 w2h[G::W2L ? 1 : G::KS2], w2l[G::W2L ? 1 : G::KS2];
-  if constexpr (G::W1L) {
-    for (int e = tid; e < 2 * G::KS1 * 64; e += NT) {   // 16-B pieces
-      const int pl = e / (G::KS1 * 64), i = e - pl * (G::KS1 * 64);
-      *reinterpret_cast<f16x8*>(sw1 + 8 * e) = *reinterpret_cast<const f16x8*>((pl ? a.w1l : a.w1h) + 8 * i);
-    }
-  }
   if constexpr (G::W2L) {
     for (int e = tid; e < 2 * G::KS2 * 64; e += NT) {   // 16-B pieces
       const int pl = e / (G::KS2 * 64), i = e - pl * (G::KS2 * 64);
@@ -361,14 +331,12 @@ __global__ void __launch_bounds__(NT, (SG<H, W, CIN, POOL>::MINB)) rbs_kernel(Re
 #pragma unroll
     for (int ks = 0; ks < G::KPT; ++ks) xco[dx][ks] = xoff<CIN>(0, nc + dx, G::KPT == 2 ? 2 * ks + h : h);
 
-  f16x8 w1h[G::W1L ? 1 : G::PF], w1l[G::W1L ? 1 : G::PF];   // GEMM 1's weight ring (PF k-steps ahead), first steps issued early
+  f16x8 w1h[G::PF], w1l[G::PF];   // GEMM 1's weight ring (PF k-steps ahead), first steps issued early
   auto gemm1_issue = [&]() {
-    if constexpr (!G::W1L) {
 #pragma unroll
-      for (int s = 0; s < G::PF; ++s) {
-        w1h[s] = rbs_frag(rw1h, s * 512, lofs);
-        w1l[s] = rbs_frag(rw1l, s * 512, lofs);
-      }
+    for (int s = 0; s < G::PF; ++s) {
+      w1h[s] = rbs_frag(rw1h, s * 512, lofs);
+      w1l[s] = rbs_frag(rw1l, s * 512, lofs);
     }
   };
   auto gemm1 = [&](int j0) -> f32x16 {
@@ -386,28 +354,12 @@ __global__ void __launch_bounds__(NT, (SG<H, W, CIN, POOL>::MINB)) rbs_kernel(Re
     };
     f16x8 nxh = *reinterpret_cast<const f16x8*>(sx + xo(0));
     f16x8 nxl = *reinterpret_cast<const f16x8*>(sx + G::XPLANE + xo(0));
-    f16x8 nbh, nbl;
-    if constexpr (G::W1L) {
-      nbh = *reinterpret_cast<const f16x8*>(sw1 + lofs);
-      nbl = *reinterpret_cast<const f16x8*>(sw1 + G::KS1 * 512 + lofs);
-    }
 #pragma unroll
     for (int s = 0; s < G::KS1; ++s) {
-      f16x8 bh, bl;
-      if constexpr (G::W1L) {
-        bh = nbh;
-        bl = nbl;
-        if (s + 1 < G::KS1) {
-          nbh = *reinterpret_cast<const f16x8*>(sw1 + (s + 1) * 512 + lofs);
-          nbl = *reinterpret_cast<const f16x8*>(sw1 + (G::KS1 + s + 1) * 512 + lofs);
-        }
-      } else {
-        bh = w1h[s % G::PF];
-        bl = w1l[s % G::PF];
-        if (s + G::PF < G::KS1) {
-          w1h[s % G::PF] = rbs_frag(rw1h, (s + G::PF) * 512, lofs);
-          w1l[s % G::PF] = rbs_frag(rw1l, (s + G::PF) * 512, lofs);
-        }
+      const f16x8 bh = w1h[s % G::PF], bl = w1l[s % G::PF];
+      if (s + G::PF < G::KS1) {
+        w1h[s % G::PF] = rbs_frag(rw1h, (s + G::PF) * 512, lofs);
+        w1l[s % G::PF] = rbs_frag(rw1l, (s + G::PF) * 512, lofs);
       }
       const f16x8 xh = nxh, xl = nxl;
       if (s + 1 < G::KS1) {
@@ -417,7 +369,7 @@ __global__ void __launch_bounds__(NT, (SG<H, W, CIN, POOL>::MINB)) rbs_kernel(Re
       acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(bl, xh, acc, 0, 0, 0);
       acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(bh, xl, acc, 0, 0, 0);
       acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(bh, xh, acc, 0, 0, 0);
-      if (RBS_SB) __builtin_amdgcn_sched_barrier(0);   // keep the register footprint: no deeper hoisting
+      __builtin_amdgcn_sched_barrier(0);   // keep the register footprint: no deeper hoisting
     }
     return acc;
   };
@@ -586,7 +538,7 @@ __global__ void __launch_bounds__(NT, (SG<H, W, CIN, POOL>::MINB)) rbs_kernel(Re
           acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(gh, xl, acc, 0, 0, 0);
           acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(gh, xh, acc, 0, 0, 0);
         }
-        if (RBS_SB) __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
     RBS_T(6);
