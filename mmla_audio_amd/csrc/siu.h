@@ -30,6 +30,7 @@ struct SiuArgs {
   float* seq;
   const float* fs;
   const float* ft;
+  uint32_t tdiv_m, tdiv_s;   // set by the launchers: row / t as a multiply-high (callers leave 0)
 };
 
 bool siu_supported(int c);

@@ -1,29 +1,32 @@
 // SpeakerIdentification res_unit without pooling (speaker_identification.py:168-190; units 2-3, 5-6,
 // 8-9 of the nine):
 //     y = x + Conv1D_b(ReLU(BN_mid(Conv1D_a(ReLU(BN_in(x))))))        Conv1D(C, 3, 'same')
-// as ONE kernel per unit.  The SI Conv1D layers run at 3-5.4 TB/s of HBM (profiles/
-// pmc_traffic_si_pipeline.json against the kernel stats): the stack is bandwidth-bound, and the
-// two-launch form moves t1 out to HBM and back (write + read) and x twice.  Here a workgroup stages
-// ROWS + 2 rows of x (BN_in + ReLU + 3xFP16 split, as conv_h3's staging), computes the ROWS rows of
-// t1 its output rows need (GEMM a), writes them back into the same LDS already BN_mid + ReLU'd and
-// split, and computes ROWS - 2 output rows (GEMM b) + bias + residual.  t1 never leaves the CU.
+// as ONE kernel per unit.  A workgroup stages ROWS + 2 rows of x (BN_in + ReLU + 3xFP16 split, as
+// conv_h3's staging), computes the ROWS rows of t1 its output rows need (GEMM a), writes them back
+// into the same LDS already BN_mid + ReLU'd and split, and computes ROWS - 2 output rows (GEMM b) +
+// bias + residual.  t1 never leaves the CU.
 //
 // The pool units (1, 4, 7: MaxPool1D(2, 'same') of x into BN_in, and the residual is the shortcut
 // Conv1D(C, 1, strides=2) of x) run the same way with POOL: x's two source rows are max-pooled while
 // staging (conv_h3's PIN) and the epilogue computes the shortcut as a small 3xFP16 GEMM per 32-row
 // tile (conv_h3's EPI_ADD_SC), so the pool unit's t1 stays on chip too.
 //
-// Bit-identical to the conv_h3 pair it replaces: the same staged operands (values and 2^4 scale),
-// the same MFMA sequence per output element (channel chunks of 32, then taps, then k-steps, the three
-// 3xFP16 products in conv_h3's order into one accumulator), the same epilogue arithmetic, and the
-// same zero rows for taps that leave a clip (conv_h3's TW = 1 zero row) or the row sequence.
+// Both GEMMs run as C^T = W^T X^T (weights the A operand): a lane's accumulator quad is 4 adjacent
+// channels of one row, so t1 goes back to LDS as 8-B hi / lo quads and the epilogue moves float4s.
+// Row -> (clip, position) by a multiply-high division (SiuArgs::tdiv_*), 32-bit offsets, the 2^4
+// operand scale folded into the BatchNorm parameters, and a running range maximum: the round-6
+// counters put this kernel at ~23 VALU per MFMA before (profiles/r6_pmc_si_pipeline_summary.txt).
+//
+// Bit-identical to the conv_h3 pair it replaces: the same staged operands (values and 2^4 scale:
+// fma(v, 16 s, 16 t) = 16 fma(v, s, t) exactly), the same MFMA sequence per output element (channel
+// chunks of 32, then taps, then k-steps, the three 3xFP16 products in conv_h3's order into one
+// accumulator; the transposed product sums the same terms in the same order), the same epilogue
+// arithmetic, and the same zero rows for taps that leave a clip (conv_h3's TW = 1 zero row).
 #include "common.h"
 #include "conv.h"
 #include "siu.h"
 
 #include <type_traits>
-
-
 
 namespace {
 
@@ -35,20 +38,45 @@ constexpr int CK = 32;                 // channel chunk (conv_h3's k order)
 constexpr int KS = CK / 16;
 constexpr int TAPS = 3;
 constexpr float ACT_SCALE = 16.0f;
-constexpr float ACT_RANGE = 65504.0f / ACT_SCALE;
+constexpr float SPLIT_MAX = 65504.0f;  // largest finite fp16 (operands are compared once scaled)
 
-MMLA_DEV float bn_relu(float v, float sc, float sh) { return fmaxf(fmaf(v, sc, sh), 0.0f); }
+MMLA_DEV __amdgpu_buffer_rsrc_t siu_rsrc(const void* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)0xffffffff, 0x00020000);
+}
+MMLA_DEV float4 ld4(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
+  return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 0));
+}
+MMLA_DEV f16x8 ldw(__amdgpu_buffer_rsrc_t r, int lofs, int u) {   // 16 B of a split weight
+  return __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(r, (uint32_t)lofs * 2u, u * 2, 0));
+}
+// x / t for x < 2^31 (SiuArgs::tdiv_m, tdiv_s from siu_fastdiv)
+MMLA_DEV uint32_t tdiv(uint32_t x, uint32_t m, uint32_t s) { return (__umulhi(x, m) + x) >> s; }
+
+// v' = max(fma(v, sc', sh'), 0) (the BN already x 2^4), split into hi / lo quads; rmax tracks the
+// largest v' (post-ReLU: never NaN, never negative)
+MMLA_DEV void bn_split4(float4 v, float4 sc, float4 sh, f16x4& h, f16x4& l, float& rmax) {
+  const float a = fmaxf(fmaf(v.x, sc.x, sh.x), 0.0f), b = fmaxf(fmaf(v.y, sc.y, sh.y), 0.0f);
+  const float c = fmaxf(fmaf(v.z, sc.z, sh.z), 0.0f), d = fmaxf(fmaf(v.w, sc.w, sh.w), 0.0f);
+  rmax = fmaxf(rmax, fmaxf(fmaxf(a, b), fmaxf(c, d)));
+  h[0] = (_Float16)a;
+  h[1] = (_Float16)b;
+  h[2] = (_Float16)c;
+  h[3] = (_Float16)d;
+  const uint2 hu = __builtin_bit_cast(uint2, h);
+  l = __builtin_bit_cast(f16x4, make_uint2(split_lo2(a, b, hu.x), split_lo2(c, d, hu.y)));
+}
 
 // CIN input / C output channels; NW waves; ROWS = t1 rows per workgroup = a multiple of the waves'
 // 32-row MFMA tiles; output rows per workgroup R = ROWS - 2 (t1 needs one row of halo each side, x
 // two).  POOL: a pool unit (rows are pooled rows, a.t_src the unpooled rows per clip)
 // FIN (the last unit): the epilogue writes BN + ReLU + AveragePooling1D(4) of the unit's output
 // (speaker_identification.py:208-212, nets.hip bn_relu_avgpool4_kernel's arithmetic) instead of the
-// output itself; tiles then hold a multiple of 4 output rows, so no pool window straddles two
+// output itself; tiles then hold a multiple of 4 output rows, so no pool window straddles two.  FIN's
+// GEMM b keeps the natural C = X W form (a lane's quad = 4 rows of one channel = one pool window).
 template <int CIN, int C, int ROWS, int NW, bool POOL, bool FIN, int MINW = 2>
 __global__ void __launch_bounds__(64 * NW, MINW) siu_kernel(SiuArgs a) {
   constexpr int NT = 64 * NW;
-  constexpr int WN = C / 32;           // waves along N (32 columns each), as conv_h3 with BN = C
+  constexpr int WN = C / 32;           // waves along N (32 channels each)
   constexpr int WM = NW / WN;
   constexpr int MT = ROWS / (WM * 32);
   constexpr int NCHX = CIN / CK;       // channel chunks of GEMM a / GEMM b
@@ -64,77 +92,67 @@ __global__ void __launch_bounds__(64 * NW, MINW) siu_kernel(SiuArgs a) {
   static_assert(POOL || CIN == C, "a unit without pooling keeps its width");
   __shared__ __attribute__((aligned(16))) _Float16 lhi[(XR + 1) * LDP];
   __shared__ __attribute__((aligned(16))) _Float16 llo[(XR + 1) * LDP];
+  // per-channel parameters: [0] b_a, [1] 16 s_mid, [2] 16 t_mid, [3] b_b, [4] the shortcut bias
+  __shared__ __attribute__((aligned(16))) float spar[5 * C];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave - (wave / WN) * WN;
-  const int64_t HH = (int64_t)a.n * a.t;
-  const int64_t r0 = (int64_t)blockIdx.x * R;
+  const int HH = a.n * a.t;                       // rows of the batch (< 2^24, siu_launch checks)
+  const int r0 = (int)blockIdx.x * R;
   const int koff = (lane >> 5) * 8;
-  bool rbad = false;
+  const int h4 = 4 * (lane >> 5);
+  const uint32_t tm = a.tdiv_m, ts = a.tdiv_s;
+  float rmax = 0.0f;                              // the largest scaled operand this thread split
+  bool rbad = false;                              // ... or a raw shortcut operand out of range / NaN
+  const __amdgpu_buffer_rsrc_t rx = siu_rsrc(a.x);
 
   if (tid < LDPX / 8) {   // the zero row (x pitch)
     *reinterpret_cast<f16x8*>(lhi + ZR * LDPX + 8 * tid) = f16x8{};
     *reinterpret_cast<f16x8*>(llo + ZR * LDPX + 8 * tid) = f16x8{};
   }
+  for (int i = tid; i < C; i += NT) {
+    spar[i] = a.ba[i];
+    spar[C + i] = ACT_SCALE * a.s_mid[i];
+    spar[2 * C + i] = ACT_SCALE * a.t_mid[i];
+    spar[3 * C + i] = a.bb[i];
+    spar[4 * C + i] = POOL ? a.bs[i] : 0.0f;
+  }
 
   // ---- stage x: rows r0 - 2 + j, BN_in + ReLU, x 2^4, split (all chunks, one barrier) ------------
-  //      (POOL: row g = (clip, tt) is the max of the clip's unpooled rows 2 tt, 2 tt + 1)
+  //      (POOL: row g = (clip, tt) is the max of the clip's unpooled rows 2 tt, 2 tt + 1).  Rows
+  //      outside the batch load row 0 / HH - 1 instead: GEMM a reaches them only through taps that
+  //      leave a clip (the zero row) or for t1 rows outside the batch, which GEMM b never reads.
   {
     const int q = tid % QPP;
 #pragma unroll 1
     for (int ch = 0; ch < NCHX; ++ch) {
       const int ci = ch * CK + 4 * q;
-      const float4 sc = *reinterpret_cast<const float4*>(a.s_in + ci);
-      const float4 sh = *reinterpret_cast<const float4*>(a.t_in + ci);
+      float4 sc = *reinterpret_cast<const float4*>(a.s_in + ci);
+      float4 sh = *reinterpret_cast<const float4*>(a.t_in + ci);
+      sc = make_float4(ACT_SCALE * sc.x, ACT_SCALE * sc.y, ACT_SCALE * sc.z, ACT_SCALE * sc.w);
+      sh = make_float4(ACT_SCALE * sh.x, ACT_SCALE * sh.y, ACT_SCALE * sh.z, ACT_SCALE * sh.w);
       float4 pre[MAXT];
-      uint32_t valid = 0;
 #pragma unroll
       for (int j = 0; j < MAXT; ++j) {
         const int task = tid + j * NT;
-        pre[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-        const int64_t g = r0 - 2 + task / QPP;
-        if (task < XR * QPP && g >= 0 && g < HH) {
-          if constexpr (POOL) {
-            const int64_t cl = g / a.t;
-            const int tt = (int)(g - cl * a.t);
-            const float* src = a.x + (cl * a.t_src + 2 * tt) * CIN + ci;
-            float4 v = *reinterpret_cast<const float4*>(src);
-            if (2 * tt + 1 < a.t_src) {
-              const float4 u = *reinterpret_cast<const float4*>(src + CIN);
-              v = make_float4(fmaxf(v.x, u.x), fmaxf(v.y, u.y), fmaxf(v.z, u.z), fmaxf(v.w, u.w));
-            }
-            pre[j] = v;
-          } else {
-            pre[j] = *reinterpret_cast<const float4*>(a.x + g * C + ci);
-          }
-          valid |= 1u << j;
+        const int g = min(max(r0 - 2 + task / QPP, 0), HH - 1);
+        if constexpr (POOL) {
+          const uint32_t cl = tdiv((uint32_t)g, tm, ts);
+          const int tt = g - (int)cl * a.t;
+          const uint32_t src = ((uint32_t)cl * (uint32_t)a.t_src + 2u * tt) * (CIN * 4u) + ci * 4u;
+          const float4 v = ld4(rx, src);
+          const float4 u = ld4(rx, 2 * tt + 1 < a.t_src ? src + CIN * 4u : src);
+          pre[j] = make_float4(fmaxf(v.x, u.x), fmaxf(v.y, u.y), fmaxf(v.z, u.z), fmaxf(v.w, u.w));
+        } else {
+          pre[j] = ld4(rx, (uint32_t)g * (C * 4u) + ci * 4u);
         }
       }
 #pragma unroll
       for (int j = 0; j < MAXT; ++j) {
         const int task = tid + j * NT;
-        if (task >= XR * QPP) continue;
-        float4 v = pre[j];
-        if (valid & (1u << j)) {
-          v.x = bn_relu(v.x, sc.x, sh.x);
-          v.y = bn_relu(v.y, sc.y, sh.y);
-          v.z = bn_relu(v.z, sc.z, sh.z);
-          v.w = bn_relu(v.w, sc.w, sh.w);
-        }
-        rbad |= !(fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))) < ACT_RANGE);
-        v.x *= ACT_SCALE;
-        v.y *= ACT_SCALE;
-        v.z *= ACT_SCALE;
-        v.w *= ACT_SCALE;
+        if (MAXT * NT > XR * QPP && task >= XR * QPP) continue;
         f16x4 hv, lv;
-        hv[0] = (_Float16)v.x;
-        hv[1] = (_Float16)v.y;
-        hv[2] = (_Float16)v.z;
-        hv[3] = (_Float16)v.w;
-        {
-          const uint2 hu_ = __builtin_bit_cast(uint2, hv);
-          lv = __builtin_bit_cast(f16x4, make_uint2(split_lo2(v.x, v.y, hu_.x), split_lo2(v.z, v.w, hu_.y)));
-        }
+        bn_split4(pre[j], sc, sh, hv, lv, rmax);
         const int row = task / QPP;
         *reinterpret_cast<f16x4*>(lhi + row * LDPX + ci) = hv;
         *reinterpret_cast<f16x4*>(llo + row * LDPX + ci) = lv;
@@ -143,21 +161,24 @@ __global__ void __launch_bounds__(64 * NW, MINW) siu_kernel(SiuArgs a) {
   }
   __syncthreads();
 
-  // B fragments (conv_h3_split_weights order): per tap, 16-channel k-step and 32-column tile
-  constexpr size_t kstride = (size_t)(C / 32) * 512;
+  // weight fragments (conv_h3_split_weights order): per tap, 16-channel k-step and 32-column tile
+  constexpr int kstride = (C / 32) * 512;
   const int lofs = wn * 512 + lane * 8;
-  // this lane's A rows and, per tap, the LDS row it reads (the zero row where the tap leaves the clip);
-  // NCHK channel chunks of A rows LDPA halfs apart
-  auto gemm = [&](auto nchk_c, auto ldpa_c, const uint16_t* __restrict__ wh,
-                  const uint16_t* __restrict__ wl, int64_t g_row0, f32x16 (&acc)[MT]) {
+  // this lane's LDS row per tile and, per tap, that row or the zero row where the tap leaves the
+  // clip; NCHK channel chunks of rows LDPA halfs apart.  CT: acc = W^T X^T (lane = row, quads of
+  // channels), else acc = X W (lane = channel, quads of rows)
+  auto gemm = [&](auto nchk_c, auto ldpa_c, auto ct_c, const uint16_t* wh, const uint16_t* wl, int g_row0,
+                  f32x16 (&acc)[MT]) {
     constexpr int NCHK = decltype(nchk_c)::value, LDPA = decltype(ldpa_c)::value;
-    constexpr size_t tap_stride = (size_t)C * NCHK * CK;
+    constexpr bool CT = decltype(ct_c)::value;
+    constexpr int tap_stride = C * NCHK * CK;
+    const __amdgpu_buffer_rsrc_t rwh = siu_rsrc(wh), rwl = siu_rsrc(wl);
     int mrow[MT], trow[MT];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
       mrow[mt] = (wm * MT + mt) * 32 + (lane & 31);
-      const int64_t g = g_row0 + mrow[mt];                 // the global row of this A row
-      trow[mt] = (int)(((g % a.t) + a.t) % a.t);           // its position in its clip
+      const uint32_t gp = (uint32_t)(g_row0 + mrow[mt] + a.t);            // >= 0
+      trow[mt] = (int)(gp - tdiv(gp, tm, ts) * (uint32_t)a.t);            // the row's position in its clip
 #pragma unroll
       for (int i = 0; i < 16; ++i) acc[mt][i] = 0.0f;
     }
@@ -168,9 +189,9 @@ __global__ void __launch_bounds__(64 * NW, MINW) siu_kernel(SiuArgs a) {
         f16x8 bh[KS], bl[KS];
 #pragma unroll
         for (int s = 0; s < KS; ++s) {
-          const size_t u = tap * tap_stride + (size_t)(ch * KS + s) * kstride + lofs;
-          bh[s] = *reinterpret_cast<const f16x8*>(wh + u);
-          bl[s] = *reinterpret_cast<const f16x8*>(wl + u);
+          const int u = tap * tap_stride + (ch * KS + s) * kstride;
+          bh[s] = ldw(rwh, lofs, u);
+          bl[s] = ldw(rwl, lofs, u);
         }
 #pragma unroll
         for (int s = 0; s < KS; ++s)
@@ -180,19 +201,24 @@ __global__ void __launch_bounds__(64 * NW, MINW) siu_kernel(SiuArgs a) {
             const int off = (src < 0 || src >= a.t ? ZR : mrow[mt] + tap) * LDPA + ch * CK + 16 * s + koff;
             const f16x8 ah = *reinterpret_cast<const f16x8*>(lhi + off);
             const f16x8 al = *reinterpret_cast<const f16x8*>(llo + off);
-            acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl[s], acc[mt], 0, 0, 0);
-            acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[s], acc[mt], 0, 0, 0);
-            acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[s], acc[mt], 0, 0, 0);
+            if constexpr (CT) {
+              acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(bl[s], ah, acc[mt], 0, 0, 0);
+              acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(bh[s], al, acc[mt], 0, 0, 0);
+              acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(bh[s], ah, acc[mt], 0, 0, 0);
+            } else {
+              acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl[s], acc[mt], 0, 0, 0);
+              acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[s], acc[mt], 0, 0, 0);
+              acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[s], acc[mt], 0, 0, 0);
+            }
           }
       }
     }
   };
 
-  const int co = wn * 32 + (lane & 31);
-  const int hsel = 4 * (lane >> 5);
   f32x16 acc[MT];
   // ---- GEMM a: t1 rows r0 - 1 + m, m < ROWS (x LDS row of t1 row m at tap dy: m + dy) -------------
-  gemm(std::integral_constant<int, NCHX>{}, std::integral_constant<int, LDPX>{}, a.wah, a.wal, r0 - 1, acc);
+  gemm(std::integral_constant<int, NCHX>{}, std::integral_constant<int, LDPX>{}, std::true_type{}, a.wah, a.wal,
+       r0 - 1, acc);
   __syncthreads();   // every wave has read x
   if constexpr (LDPX != LDP) {   // the zero row again, in t1's pitch
     if (tid < LDP / 8) {
@@ -201,131 +227,158 @@ __global__ void __launch_bounds__(64 * NW, MINW) siu_kernel(SiuArgs a) {
     }
   }
   {
-    const float b = a.ba[co], s2 = a.s_mid[co], t2 = a.t_mid[co];
+    // lane: t1 row m (its tile's lane & 31), channels co0 + 0..3 of each quad q
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
+    for (int mt = 0; mt < MT; ++mt) {
+      const int m = (wm * MT + mt) * 32 + (lane & 31);
+      const int g = r0 - 1 + m;
+      float tmax = 0.0f;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = (wm * MT + mt) * 32 + (r & 3) + 8 * (r >> 2) + hsel;
-        const int64_t g = r0 - 1 + m;
-        float v = 0.0f;
-        if (g >= 0 && g < HH) {   // rows outside the sequence stage as zeros (conv_h3's valid mask)
-          v = bn_relu(fmaf(acc[mt][r], a.ua, b), s2, t2);
-          rbad |= !(fabsf(v) < ACT_RANGE);
-        }
-        v *= ACT_SCALE;
-        const _Float16 hv = (_Float16)v;
-        lhi[m * LDP + co] = hv;
-        llo[m * LDP + co] = (_Float16)(v - (float)hv);
+      for (int q = 0; q < 4; ++q) {
+        const int co0 = wn * 32 + 8 * q + h4;
+        const float4 b = *reinterpret_cast<const float4*>(spar + co0);
+        const float4 s2 = *reinterpret_cast<const float4*>(spar + C + co0);
+        const float4 t2 = *reinterpret_cast<const float4*>(spar + 2 * C + co0);
+        const float4 v = make_float4(fmaf(acc[mt][4 * q], a.ua, b.x), fmaf(acc[mt][4 * q + 1], a.ua, b.y),
+                                     fmaf(acc[mt][4 * q + 2], a.ua, b.z), fmaf(acc[mt][4 * q + 3], a.ua, b.w));
+        f16x4 hv, lv;
+        bn_split4(v, s2, t2, hv, lv, tmax);
+        *reinterpret_cast<f16x4*>(lhi + m * LDP + co0) = hv;
+        *reinterpret_cast<f16x4*>(llo + m * LDP + co0) = lv;
       }
+      // t1 rows outside the batch are never read (see staging): kept out of the range guard
+      if (g >= 0 && g < HH) rmax = fmaxf(rmax, tmax);
+    }
   }
   __syncthreads();
   // ---- GEMM b: output rows r0 + m, m < R (t1 LDS row of output row m at tap dy: m + dy) -----------
-  // EARLY: the residuals of all MT tiles loaded before GEMM b, so their latency hides under it
-  // (units without pooling whose registers allow it: MT 2)
-  constexpr bool EARLY = !POOL && MT <= 2;
-  float ersd[EARLY ? MT : 1][16];
-  if constexpr (EARLY) {
+  if constexpr (!FIN) {
+    // EARLY: the residuals of all MT tiles loaded before GEMM b, so their latency hides under it
+    // (units without pooling whose registers allow it: MT 2)
+    constexpr bool EARLY = !POOL && MT <= 2;
+    float4 ersd[EARLY ? MT : 1][4];
+    auto rsd_off = [&](int mt, int q) {
+      const int g = min(r0 + (wm * MT + mt) * 32 + (lane & 31), HH - 1);
+      return (uint32_t)g * (C * 4u) + (wn * 32 + 8 * q + h4) * 4u;
+    };
+    if constexpr (EARLY) {
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
+      for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = (wm * MT + mt) * 32 + (r & 3) + 8 * (r >> 2) + hsel;
-        const int64_t g = r0 + m;
-        ersd[mt][r] = m < R && g < HH ? a.x[g * C + co] : 0.0f;
-      }
-  }
-  gemm(std::integral_constant<int, NCH>{}, std::integral_constant<int, LDP>{}, a.wbh, a.wbl, r0, acc);
-  {
-    const float b = a.bb[co];
+        for (int q = 0; q < 4; ++q) ersd[mt][q] = ld4(rx, rsd_off(mt, q));
+    }
+    gemm(std::integral_constant<int, NCH>{}, std::integral_constant<int, LDP>{}, std::true_type{}, a.wbh, a.wbl, r0,
+         acc);
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {   // one 32-row tile at a time: 16 residuals live, not 16 MT
-      float rsd[16];
+      const int m = (wm * MT + mt) * 32 + (lane & 31);
+      const int g = r0 + m;
+      float4 rsd[4];
       if constexpr (POOL) {
-        // the shortcut Conv1D(1, stride 2) of x as conv_h3's EPI_ADD_SC: A row = the output row's
-        // source row 2 tt of x (raw, x 2^4, split), 16-channel k-steps, its own accumulator
+        // the shortcut Conv1D(1, stride 2) of x as conv_h3's EPI_ADD_SC: the row's source row 2 tt of
+        // x (raw, x 2^4, split) is the B operand, 16-channel k-steps, its own accumulator
         f32x16 sacc;
 #pragma unroll
         for (int i = 0; i < 16; ++i) sacc[i] = 0.0f;
-        const int64_t g = r0 + (wm * MT + mt) * 32 + (lane & 31);
-        const bool sok = g < HH;
-        const int64_t gs = sok ? g : 0;
-        const int64_t cl = gs / a.t;
-        const int tt = (int)(gs - cl * a.t);
-        const float* sxp = a.x + (cl * a.t_src + 2 * tt) * CIN + koff;
+        const int gs = min(g, HH - 1);
+        const uint32_t cl = tdiv((uint32_t)gs, tm, ts);
+        const int tt = gs - (int)cl * a.t;
+        const uint32_t sxo = ((uint32_t)cl * (uint32_t)a.t_src + 2u * tt) * (CIN * 4u) + koff * 4u;
+        const __amdgpu_buffer_rsrc_t rsh = siu_rsrc(a.wsh), rsl = siu_rsrc(a.wsl);
 #pragma unroll
         for (int s = 0; s < CIN / 16; ++s) {
-          const f16x8 sbh = *reinterpret_cast<const f16x8*>(a.wsh + (size_t)s * kstride + lofs);
-          const f16x8 sbl = *reinterpret_cast<const f16x8*>(a.wsl + (size_t)s * kstride + lofs);
-          float4 x0 = make_float4(0.f, 0.f, 0.f, 0.f), x1 = x0;
-          if (sok) {
-            x0 = *reinterpret_cast<const float4*>(sxp + 16 * s);
-            x1 = *reinterpret_cast<const float4*>(sxp + 16 * s + 4);
-          }
+          const f16x8 sbh = ldw(rsh, lofs, s * kstride);
+          const f16x8 sbl = ldw(rsl, lofs, s * kstride);
+          const float4 x0 = ld4(rx, sxo + 64u * s), x1 = ld4(rx, sxo + 64u * s + 16u);
           const float xv[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
           f16x8 xh, xl;
 #pragma unroll
           for (int k = 0; k < 8; ++k) {
-            rbad |= !(fabsf(xv[k]) < ACT_RANGE);
             const float v = xv[k] * ACT_SCALE;
+            rbad |= !(fabsf(v) < SPLIT_MAX);
             xh[k] = (_Float16)v;
             xl[k] = (_Float16)(v - (float)xh[k]);
           }
-          sacc = __builtin_amdgcn_mfma_f32_32x32x16_f16(xh, sbl, sacc, 0, 0, 0);
-          sacc = __builtin_amdgcn_mfma_f32_32x32x16_f16(xl, sbh, sacc, 0, 0, 0);
-          sacc = __builtin_amdgcn_mfma_f32_32x32x16_f16(xh, sbh, sacc, 0, 0, 0);
+          sacc = __builtin_amdgcn_mfma_f32_32x32x16_f16(sbl, xh, sacc, 0, 0, 0);
+          sacc = __builtin_amdgcn_mfma_f32_32x32x16_f16(sbh, xl, sacc, 0, 0, 0);
+          sacc = __builtin_amdgcn_mfma_f32_32x32x16_f16(sbh, xh, sacc, 0, 0, 0);
         }
-        const float bsc = a.bs[co];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) rsd[r] = fmaf(sacc[r], a.us, bsc);
-      } else {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int m = (wm * MT + mt) * 32 + (r & 3) + 8 * (r >> 2) + hsel;
-          const int64_t g = r0 + m;
-          rsd[r] = EARLY ? ersd[EARLY ? mt : 0][r] : (m < R && g < HH ? a.x[g * C + co] : 0.0f);
-        }
-      }
-      if constexpr (FIN) {
-        // registers 4 q .. 4 q + 3 are the rows m0 .. m0 + 3, m0 = 8 q + hsel (+ tile): with r0, R
-        // and t multiples of 4 each group is one pool window of one clip
-        const float fs = a.fs[co], ft = a.ft[co];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const int m0 = (wm * MT + mt) * 32 + 8 * q + hsel;
-          const int64_t g0 = r0 + m0;
-          if (m0 < R && g0 < HH) {
-            float sum = 0.0f;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              float val = fmaf(acc[mt][4 * q + j], a.ub, b);
-              val += rsd[4 * q + j];
-              sum += fmaxf(fmaf(val, fs, ft), 0.0f);
-            }
-            a.seq[(g0 >> 2) * C + co] = sum / 4.0f;
-          }
+          const float4 bs = *reinterpret_cast<const float4*>(spar + 4 * C + wn * 32 + 8 * q + h4);
+          rsd[q] = make_float4(fmaf(sacc[4 * q], a.us, bs.x), fmaf(sacc[4 * q + 1], a.us, bs.y),
+                               fmaf(sacc[4 * q + 2], a.us, bs.z), fmaf(sacc[4 * q + 3], a.us, bs.w));
         }
       } else {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int m = (wm * MT + mt) * 32 + (r & 3) + 8 * (r >> 2) + hsel;
-          const int64_t g = r0 + m;
-          if (m < R && g < HH) {
-            float val = fmaf(acc[mt][r], a.ub, b);
-            val += rsd[r];
-            a.y[g * C + co] = val;
+        for (int q = 0; q < 4; ++q) rsd[q] = EARLY ? ersd[EARLY ? mt : 0][q] : ld4(rx, rsd_off(mt, q));
+      }
+      if (m < R && g < HH) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int co0 = wn * 32 + 8 * q + h4;
+          const float4 b = *reinterpret_cast<const float4*>(spar + 3 * C + co0);
+          float4 val = make_float4(fmaf(acc[mt][4 * q], a.ub, b.x), fmaf(acc[mt][4 * q + 1], a.ub, b.y),
+                                   fmaf(acc[mt][4 * q + 2], a.ub, b.z), fmaf(acc[mt][4 * q + 3], a.ub, b.w));
+          val.x += rsd[q].x;
+          val.y += rsd[q].y;
+          val.z += rsd[q].z;
+          val.w += rsd[q].w;
+          *reinterpret_cast<float4*>(a.y + (size_t)g * C + co0) = val;
+        }
+      }
+    }
+  } else {
+    static_assert(!FIN || (!POOL && CIN == C), "the last unit keeps its width");
+    gemm(std::integral_constant<int, NCH>{}, std::integral_constant<int, LDP>{}, std::false_type{}, a.wbh, a.wbl, r0,
+         acc);
+    const int co = wn * 32 + (lane & 31);
+    const float b = spar[3 * C + co], fs = a.fs[co], ft = a.ft[co];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      // registers 4 q .. 4 q + 3 are the rows m0 .. m0 + 3, m0 = 8 q + h4 (+ tile): with r0, R and t
+      // multiples of 4 each group is one pool window of one clip
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int m0 = (wm * MT + mt) * 32 + 8 * q + h4;
+        const int g0 = r0 + m0;
+        float rs[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          rs[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                rx, (uint32_t)min(g0 + j, HH - 1) * (C * 4u) + co * 4u, 0, 0));
+        if (m0 < R && g0 < HH) {
+          float sum = 0.0f;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            float val = fmaf(acc[mt][4 * q + j], a.ub, b);
+            val += rs[j];
+            sum += fmaxf(fmaf(val, fs, ft), 0.0f);
           }
+          a.seq[(size_t)(g0 >> 2) * C + co] = sum / 4.0f;
         }
       }
     }
   }
-  if (rbad && a.range_flag) *a.range_flag = 1;
+  if ((rbad || !(rmax < SPLIT_MAX)) && a.range_flag) *a.range_flag = 1;
+}
+
+// q = x / d for x < 2^31 as (umulhi(x, m) + x) >> s: s = ceil(log2 d), m = floor(2^(32+s) / d) + 1 - 2^32
+void siu_fastdiv(uint32_t d, uint32_t& m, uint32_t& s) {
+  s = 0;
+  while ((1u << s) < d) ++s;
+  m = (uint32_t)(((uint64_t)1 << (32 + s)) / d + 1 - ((uint64_t)1 << 32));
 }
 
 template <int CIN, int C, int ROWS, int NW, bool POOL = false, bool FIN = false, int MINW = 2>
-hipError_t launch(const SiuArgs& a, hipStream_t s) {
+hipError_t launch(const SiuArgs& a0, hipStream_t s) {
   constexpr int R = FIN ? (ROWS - 2) / 4 * 4 : ROWS - 2;
+  SiuArgs a = a0;
+  siu_fastdiv((uint32_t)a.t, a.tdiv_m, a.tdiv_s);
   const int64_t rows = (int64_t)a.n * a.t;
+  // 32-bit row indices and byte offsets: x (pool units: [n t_src, CIN]) and y below 4 GiB
+  const int64_t xbytes = (int64_t)a.n * (POOL ? a.t_src : a.t) * CIN * 4;
+  if (rows >= (1 << 24) || xbytes > 0xffffff00ll || rows * C * 4 > 0xffffff00ll) return hipErrorInvalidValue;
   const int64_t blocks = (rows + R - 1) / R;
   hipLaunchKernelGGL((siu_kernel<CIN, C, ROWS, NW, POOL, FIN, MINW>), dim3((unsigned)blocks), dim3(64 * NW), 0, s, a);
   return hipGetLastError();
@@ -363,13 +416,11 @@ hipError_t siu_launch(const SiuArgs& a, int c, hipStream_t s) {
     return launch<128, 128, 128, 4, false, true>(a, s);
   }
   if (!a.x || !a.y || a.x == a.y || a.t < 1) return hipErrorInvalidValue;
-  // Tiles (4 waves): C = 32 256 t1 rows (MT 2, 134 VGPRs, 3 workgroups per CU); C = 64 256 rows and
-  // C = 128 128 rows (MT 4, 242 VGPRs once the residual epilogue went tile by tile, 2 per CU).
-  // Measured per unit and SI step against the conv_h3 pair: C = 32 1.004 vs 1.033 ms, C = 64 (128-row
-  // tiles) 1.061 vs 1.203 ms, C = 128 with 64-row tiles 1.672 vs 1.625 ms (B streamed per 62 output
-  // rows); with the MT 4 tiles SI 2.45 -> 2.51 M clips/s (A/B, 2 rounds; the conv stage itself
-  // +0.8 %).  Tried: 8-wave workgroups
-  // (one per CU) and 512-row C = 32 tiles (occupancy 1): slower
+  // Tiles (4 waves): C = 32 256 t1 rows (MT 2, 3 workgroups per CU); C = 64 256 rows and C = 128
+  // 128 rows (MT 4, 2 per CU).  Measured per unit and SI step against the conv_h3 pair (round 4):
+  // C = 32 1.004 vs 1.033 ms, C = 64 (128-row tiles) 1.061 vs 1.203 ms, C = 128 with 64-row tiles
+  // 1.672 vs 1.625 ms (B streamed per 62 output rows).  Tried: 8-wave workgroups (one per CU) and
+  // 512-row C = 32 tiles (occupancy 1): slower
   if (c == 32) return launch<32, 32, 256, 4>(a, s);
   if (c == 64) return launch<64, 64, 256, 4>(a, s);
   if (c == 128) return launch<128, 128, 128, 4>(a, s);
