@@ -18,6 +18,18 @@ MMLA_DEV uint32_t split_lo2(float a, float b, uint32_t hi) {
   return lo;
 }
 
+// 16 ELU(u) from u16 = 16 u (TF Elu: exp(x) - 1 for x < 0; the power-of-two scaling commutes with every
+// rounding).  With e = 16 exp(u) - 16: u > 0 gives 0 < u < e (or e = inf), u <= 0 gives u <= e <= 0,
+// so ELU is the median of (u, e, 0) -- one v_med3 instead of a compare and a select.  (Where the
+// rounding of e puts it a hair below u, for |u16| ~ 1e-3, the median returns u: within 1e-6.)  Every
+// 3xFP16 ELU (rbs, odu, conv_h3's PRO_BN_ELU) uses it, so the fused kernels stay bit-identical to the
+// conv_h3 launches they replace.
+MMLA_DEV float elu16(float u16) {
+  constexpr float L2E_16 = 1.4426950408889634f / 16.0f;   // log2(e) / 2^4
+  const float e = fmaf(__builtin_amdgcn_exp2f(u16 * L2E_16), 16.0f, -16.0f);
+  return __builtin_amdgcn_fmed3f(u16, e, 0.0f);
+}
+
 // XCD-aware workgroup order (MI355X_MICROARCH.md, workgroup dispatch): blocks b and b + 8 share an
 // XCD's L2, so the logical id handed to a kernel puts consecutive ids on one XCD -- neighbouring
 // tiles of one clip, whose input halos overlap, then meet in the same L2.  Bijective for any count.

@@ -69,8 +69,9 @@ MMLA_DEV float pro_fn(float v, float sc, float sh) {
     return v;
   } else {
     v = fmaf(v, sc, sh);
-    // Keras/TF Elu: exp(x) - 1 for x < 0 (Eigen: (x < 0).select(x.exp() - 1, x))
-    if constexpr (PRO == PRO_BN_ELU) return v > 0.0f ? v : __expf(v) - 1.0f;
+    // Keras/TF Elu: exp(x) - 1 for x < 0 (Eigen: (x < 0).select(x.exp() - 1, x)), as elu16 (exact
+    // power-of-two scalings) so odu / rbs reproduce these operands bit for bit
+    if constexpr (PRO == PRO_BN_ELU) return elu16(16.0f * v) * 0.0625f;
     return fmaxf(v, 0.0f);
   }
 }

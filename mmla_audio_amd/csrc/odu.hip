@@ -37,7 +37,7 @@ typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 constexpr int CK = 32;                 // channel chunk (conv_h3's k order)
 constexpr int KS = CK / 16;            // MFMA k-steps per chunk
 constexpr float ACT_SCALE = 16.0f;     // 2^4, as conv_h3
-constexpr float ACT_RANGE = 65504.0f / ACT_SCALE;
+constexpr float SPLIT_MAX = 65504.0f;  // largest finite fp16 (operands are compared once scaled)
 
 MMLA_DEV __amdgpu_buffer_rsrc_t odu_rsrc(const void* p) {
   const uint64_t u = reinterpret_cast<uint64_t>(p);
@@ -51,17 +51,12 @@ MMLA_DEV f16x8 odu_frag(__amdgpu_buffer_rsrc_t r, size_t uoff, int lofs) {
   return __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(r, (uint32_t)lofs * 2u, (int)(uoff * 2), 0));
 }
 
-// conv_h3's PRO_BN_ELU prologue (Keras/TF Elu: exp(x) - 1 for x < 0)
-MMLA_DEV float bn_elu(float v, float sc, float sh) {
-  v = fmaf(v, sc, sh);
-  return v > 0.0f ? v : __expf(v) - 1.0f;
-}
+// conv_h3's PRO_BN_ELU prologue x 2^4 (sc16, sh16 = 2^4 x the folded BatchNorm: exact)
+MMLA_DEV float bn_elu16(float v, float sc16, float sh16) { return elu16(fmaf(v, sc16, sh16)); }
+MMLA_DEV float4 x16(float4 v) { return make_float4(ACT_SCALE * v.x, ACT_SCALE * v.y, ACT_SCALE * v.z, ACT_SCALE * v.w); }
 
+// v (already x 2^4) = hi + lo, both fp16
 MMLA_DEV void split4(float4 v, f16x4& h, f16x4& l) {
-  v.x *= ACT_SCALE;
-  v.y *= ACT_SCALE;
-  v.z *= ACT_SCALE;
-  v.w *= ACT_SCALE;
   h[0] = (_Float16)v.x;
   h[1] = (_Float16)v.y;
   h[2] = (_Float16)v.z;
@@ -70,8 +65,9 @@ MMLA_DEV void split4(float4 v, f16x4& h, f16x4& l) {
   l = __builtin_bit_cast(f16x4, make_uint2(split_lo2(v.x, v.y, hu.x), split_lo2(v.z, v.w, hu.y)));
 }
 
-MMLA_DEV bool in_range4(float4 v) {
-  return fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))) < ACT_RANGE;
+// the running range maximum of split operands (ResBlkArgs / OduArgs::range_flag)
+MMLA_DEV float amax4(float r, float4 v) {
+  return fmaxf(r, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
 }
 
 // H x W image, CIN -> C channels, strips of TW columns, 4 waves: WN = C / 32 waves along the output
@@ -124,7 +120,7 @@ __global__ void __launch_bounds__(64 * NW, MINW) odu_kernel(OduArgs a) {
   const int cob = wn * 32;                    // this wave's output-channel tile
   const int lofs = wn * 512 + lane * 8;       // its B fragment inside a (tap, k-step) 1 KB block
   constexpr size_t kstr = (size_t)(C / 32) * 512;
-  bool rbad = false;
+  float rmax = 0.0f;   // the largest |operand| this thread split (x 2^4)
 
   int mpix[MT];   // the wave's pixels (C^T columns / pixel rows): strip pixel m = i * TW + c
 #pragma unroll
@@ -147,8 +143,8 @@ __global__ void __launch_bounds__(64 * NW, MINW) odu_kernel(OduArgs a) {
     // global loads of chunk ch's halo quads, then BN_in + ELU + 2^4 + split into halo buffer buf
     auto load_stage = [&](int ch, int buf) {
       const int ci = ch * CK + 4 * q;
-      const float4 sc = *reinterpret_cast<const float4*>(a.s_in + ci);
-      const float4 sh = *reinterpret_cast<const float4*>(a.t_in + ci);
+      const float4 sc = x16(*reinterpret_cast<const float4*>(a.s_in + ci));
+      const float4 sh = x16(*reinterpret_cast<const float4*>(a.t_in + ci));
       float4 pre[MAXT];
       uint32_t valid = 0;
 #pragma unroll
@@ -168,12 +164,12 @@ __global__ void __launch_bounds__(64 * NW, MINW) odu_kernel(OduArgs a) {
         if (task >= NXP * QPP) continue;
         float4 v = pre[j];
         if (valid & (1u << j)) {
-          v.x = bn_elu(v.x, sc.x, sh.x);
-          v.y = bn_elu(v.y, sc.y, sh.y);
-          v.z = bn_elu(v.z, sc.z, sh.z);
-          v.w = bn_elu(v.w, sc.w, sh.w);
+          v.x = bn_elu16(v.x, sc.x, sh.x);
+          v.y = bn_elu16(v.y, sc.y, sh.y);
+          v.z = bn_elu16(v.z, sc.z, sh.z);
+          v.w = bn_elu16(v.w, sc.w, sh.w);
         }
-        rbad |= !in_range4(v);
+        rmax = amax4(rmax, v);
         f16x4 hv, lv;
         split4(v, hv, lv);
         const int px = task / QPP;
@@ -253,20 +249,20 @@ __global__ void __launch_bounds__(64 * NW, MINW) odu_kernel(OduArgs a) {
   for (int qd = 0; qd < 4; ++qd) {
     const int c0 = cob + 8 * qd + hsel;   // the accumulator quad's 4 consecutive channels
     const float4 b4 = *reinterpret_cast<const float4*>(a.ba + c0);
-    const float4 s4 = *reinterpret_cast<const float4*>(a.s_mid + c0);
-    const float4 t4 = *reinterpret_cast<const float4*>(a.t_mid + c0);
+    const float4 s4 = x16(*reinterpret_cast<const float4*>(a.s_mid + c0));
+    const float4 t4 = x16(*reinterpret_cast<const float4*>(a.t_mid + c0));
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
       const int m = mpix[mt];
       const int i = m / TW, c = m % TW;
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
       if (w0 + c < W) {
-        v.x = bn_elu(fmaf(acc[mt][4 * qd + 0], a.ua, b4.x), s4.x, t4.x);
-        v.y = bn_elu(fmaf(acc[mt][4 * qd + 1], a.ua, b4.y), s4.y, t4.y);
-        v.z = bn_elu(fmaf(acc[mt][4 * qd + 2], a.ua, b4.z), s4.z, t4.z);
-        v.w = bn_elu(fmaf(acc[mt][4 * qd + 3], a.ua, b4.w), s4.w, t4.w);
+        v.x = bn_elu16(fmaf(acc[mt][4 * qd + 0], a.ua, b4.x), s4.x, t4.x);
+        v.y = bn_elu16(fmaf(acc[mt][4 * qd + 1], a.ua, b4.y), s4.y, t4.y);
+        v.z = bn_elu16(fmaf(acc[mt][4 * qd + 2], a.ua, b4.z), s4.z, t4.z);
+        v.w = bn_elu16(fmaf(acc[mt][4 * qd + 3], a.ua, b4.w), s4.w, t4.w);
       }
-      rbad |= !in_range4(v);
+      rmax = amax4(rmax, v);
       f16x4 hv, lv;
       split4(v, hv, lv);
       const int px = (i + 1) * TW + c;
@@ -393,7 +389,9 @@ __global__ void __launch_bounds__(64 * NW, MINW) odu_kernel(OduArgs a) {
           x0 = *reinterpret_cast<const float4*>(sx + 16 * s);
           x1 = *reinterpret_cast<const float4*>(sx + 16 * s + 4);
         }
-        rbad |= !(in_range4(x0) && in_range4(x1));
+        x0 = x16(x0);
+        x1 = x16(x1);
+        rmax = amax4(amax4(rmax, x0), x1);
         f16x4 h0, l0, h1, l1;
         split4(x0, h0, l0);
         split4(x1, h1, l1);
@@ -423,7 +421,7 @@ __global__ void __launch_bounds__(64 * NW, MINW) odu_kernel(OduArgs a) {
         a.y[((clip * (H / 2) + i0 / 2) * (W / 2) + w0 / 2) * C + co] = mx;
       }
   }
-  if (rbad && a.range_flag) *a.range_flag = 1;
+  if (!(rmax < SPLIT_MAX) && a.range_flag) *a.range_flag = 1;
 }
 
 template <int H, int W, int CIN, int C, int TW, bool POOL, int NW = 4, int MINW = 2>

@@ -47,7 +47,6 @@ constexpr int NT = 256;            // 4 waves
 constexpr int TW = 16;             // strip width (output columns)
 constexpr int R = 8;               // output rows per chunk (4 waves x 2 rows)
 constexpr int C = 32;              // output channels of blocks 1-3
-constexpr float L2E_16 = 1.4426950408889634f / 16.0f;   // log2(e) / 2^4
 constexpr float SPLIT_MAX = 65504.0f;                    // largest finite fp16
 #ifndef RBS_TRACE
 #define RBS_TRACE 0
@@ -73,15 +72,6 @@ MMLA_DEV __amdgpu_buffer_rsrc_t rbs_rsrc(const void* p) {
 // 16 B of a split weight (conv_h3_split_weights order): wave-uniform half index u + this lane's lofs
 MMLA_DEV f16x8 rbs_frag(__amdgpu_buffer_rsrc_t r, int u, int lofs) {
   return __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(r, (uint32_t)lofs * 2u, u * 2, 0));
-}
-
-// 16 ELU(u) from u16 = 16 u (TF Elu: exp(x) - 1 for x < 0; the power-of-two scaling commutes with every
-// rounding).  With e = 16 exp(u) - 16: u > 0 gives 0 < u < e (or e = inf), u <= 0 gives u <= e <= 0,
-// so ELU is the median of (u, e, 0) -- one v_med3 instead of a compare and a select.  (Where the
-// rounding of e puts it a hair below u, for |u16| ~ 1e-3, the median returns u: within 1e-6.)
-MMLA_DEV float elu16(float u16) {
-  const float e = fmaf(__builtin_amdgcn_exp2f(u16 * L2E_16), 16.0f, -16.0f);
-  return __builtin_amdgcn_fmed3f(u16, e, 0.0f);
 }
 
 // v' (already x 2^4) = hi + lo, both fp16 (RNE); lo = f16(v' - hi) exactly rounded once (v_fma_mix)
