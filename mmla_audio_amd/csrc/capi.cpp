@@ -135,6 +135,9 @@ struct mmla_ctx {
   // ... and the last one with the final BN + ReLU + AvgPool4 (siu.hip FIN); env MMLA_NO_SIFIN=1: the
   // unit writes its output and bn_relu_avgpool4 runs as its own launch
   bool sifin = true;
+  // ... and two consecutive units without pooling (2-3, 5-6, 8-9) as one kernel (siu.hip
+  // siu_pair_kernel: the first unit's output stays on chip); env MMLA_NO_SIPAIR=1: one launch each
+  bool sipair = true;
   // fused SI pipeline: si_fe writes 40-float feature rows for the stem (env MMLA_NO_SIPAD=1: 39)
   bool si_pad_feat = true;
   // OD blocks 4-9 as one fused kernel each (odu.hip: t1 on chip); env MMLA_NO_ODU=1 at create: the
@@ -1098,6 +1101,34 @@ int run_od_net(mmla_ctx* c, const uint8_t* img_u8, const float* img_f32, int64_t
   return MMLA_OK;
 }
 
+// a res unit without pooling that siu.hip runs (3xFP16 weights of the exact widths)
+bool siu_ok(const SiUnit& U, int cin) {
+  return U.ca.wh && U.cb.wh && siu_supported(cin) && U.ca.cin == cin && U.ca.cout == cin && U.cb.cin == cin &&
+         U.cb.cout == cin && U.ca.cin_pad == cin && U.ca.cout_pad == cin && U.cb.cout_pad == cin;
+}
+
+SiuArgs siu_args(const SiUnit& U, const float* x, float* y, int64_t n, int t, int* range_flag) {
+  SiuArgs s{};
+  s.n = (int)n;
+  s.t = t;
+  s.range_flag = range_flag;
+  s.x = x;
+  s.y = y;
+  s.wah = U.ca.wh;
+  s.wal = U.ca.wl;
+  s.wbh = U.cb.wh;
+  s.wbl = U.cb.wl;
+  s.ba = U.ca.bias;
+  s.bb = U.cb.bias;
+  s.s_in = U.bn_in.scale;
+  s.t_in = U.bn_in.shift;
+  s.s_mid = U.bn_mid.scale;
+  s.t_mid = U.bn_mid.shift;
+  s.ua = U.ca.unscale();
+  s.ub = U.cb.unscale();
+  return s;
+}
+
 // ldx: the features' row stride (39, or 40 from si_fe with a zero 40th column: the stem then stages
 // 16-B aligned rows, conv_h3's float4 path, bit-identical -- its weights' padded channels are zero)
 int run_si_net(mmla_ctx* c, const float* x, int64_t n, float* probs, int32_t* argmax,
@@ -1183,38 +1214,30 @@ int run_si_net(mmla_ctx* c, const float* x, int64_t n, float* probs, int32_t* ar
       }
       std::swap(X, R);
       t = tp;
-    } else if (c->siu && c->precision == MMLA_PREC_F16X3 && U.ca.wh && U.cb.wh && siu_supported(cin) &&
-               U.ca.cout == cin && U.cb.cin == cin && U.cb.cout == cin && U.ca.cin_pad == cin &&
-               U.ca.cout_pad == cin && U.cb.cout_pad == cin) {
+    } else if (c->siu && c->precision == MMLA_PREC_F16X3 && siu_ok(U, cin)) {
       // the whole unit in one launch, t1 kept on chip (siu.hip), bit-identical to the pair below
-      SiuArgs s{};
-      s.x = X;
-      s.y = R;
-      s.wah = U.ca.wh;
-      s.wal = U.ca.wl;
-      s.wbh = U.cb.wh;
-      s.wbl = U.cb.wl;
-      s.ba = U.ca.bias;
-      s.bb = U.cb.bias;
-      s.s_in = U.bn_in.scale;
-      s.t_in = U.bn_in.shift;
-      s.s_mid = U.bn_mid.scale;
-      s.t_mid = U.bn_mid.shift;
-      s.ua = U.ca.unscale();
-      s.ub = U.cb.unscale();
-      s.n = (int)n;
-      s.t = t;
-      s.range_flag = c->range_ptr;
-      if (u == 8 && c->sifin && siu_final_supported(cin) && cin == 128 && t % 4 == 0) {
+      SiuArgs s = siu_args(U, X, R, n, t, c->range_ptr);
+      SiuArgs s2{};
+      const bool pair = c->sipair && u + 1 < 9 && !POOL[u + 1] && siu_pair_supported(cin) &&
+                        siu_ok(W.unit[u + 1], cin);
+      if (pair) s2 = siu_args(W.unit[u + 1], nullptr, R, n, t, c->range_ptr);
+      SiuArgs& last = pair ? s2 : s;
+      if (u + (pair ? 1 : 0) == 8 && c->sifin && siu_final_supported(cin) && cin == 128 && t % 4 == 0) {
         // + the final BN + ReLU + AveragePooling1D(4) in the epilogue: the unit's output never
         // reaches HBM (bit-identical to bn_relu_avgpool4_launch below)
-        s.y = nullptr;
-        s.seq = static_cast<float*>(pseq);
-        s.fs = W.final_bn.scale;
-        s.ft = W.final_bn.shift;
+        last.y = nullptr;
+        last.seq = static_cast<float*>(pseq);
+        last.fs = W.final_bn.scale;
+        last.ft = W.final_bn.shift;
         fused_final = true;
       }
-      LAUNCH(c, MMLA_STAGE_CONV, 2.0 * 2.0 * n * t * 3 * cin * cin, siu_launch(s, cin, c->stream));
+      if (pair) {
+        s.y = nullptr;
+        LAUNCH(c, MMLA_STAGE_CONV, 2.0 * 2.0 * 2.0 * n * t * 3 * cin * cin, siu_pair_launch(s, s2, cin, c->stream));
+        ++u;
+      } else {
+        LAUNCH(c, MMLA_STAGE_CONV, 2.0 * 2.0 * n * t * 3 * cin * cin, siu_launch(s, cin, c->stream));
+      }
       std::swap(X, R);
     } else {
       CHK(conv_spatial(c, U.ca, X, T1, (int)n, t, 1, &U.bn_in, PRO_BN_RELU, EPI_BIAS, nullptr));
@@ -1378,6 +1401,7 @@ int mmla_create(int device, mmla_ctx** out) {
   if (const char* su = std::getenv("MMLA_NO_SIU")) c->siu = std::atoi(su) == 0;
   if (const char* sp = std::getenv("MMLA_NO_SIPU")) c->sipu = std::atoi(sp) == 0;
   if (const char* sf = std::getenv("MMLA_NO_SIFIN")) c->sifin = std::atoi(sf) == 0;
+  if (const char* sq = std::getenv("MMLA_NO_SIPAIR")) c->sipair = std::atoi(sq) == 0;
   if (const char* ls = std::getenv("MMLA_NO_LSTM_SPLIT")) c->lstm_split = std::atoi(ls) == 0;
   if (const char* lm = std::getenv("MMLA_LSTM_SPLIT_MAX")) c->lstm_split_max = std::atoi(lm);
   if (const char* sp = std::getenv("MMLA_DEBUG_LSTM_SPIN")) c->lstm_spin = std::atoi(sp);

@@ -36,6 +36,10 @@ struct SiuArgs {
 bool siu_supported(int c);
 bool siu_final_supported(int c);
 hipError_t siu_launch(const SiuArgs& a, int c, hipStream_t stream);
+// two consecutive units without pooling (a then b, b.x / a.y unused: the intermediate stays on chip);
+// b.seq set: b is the last unit (siu_final_supported's epilogue)
+bool siu_pair_supported(int c);
+hipError_t siu_pair_launch(const SiuArgs& a, const SiuArgs& b, int c, hipStream_t stream);
 // the pool unit (speaker_identification.py:170-172 + 173-188) with t1 kept on chip
 bool sipu_supported(int cin, int c);
 hipError_t sipu_launch(const SiuArgs& a, int cin, int c, hipStream_t stream);

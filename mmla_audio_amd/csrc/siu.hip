@@ -363,6 +363,258 @@ __global__ void __launch_bounds__(64 * NW, MINW) siu_kernel(SiuArgs a) {
   if ((rbad || !(rmax < SPLIT_MAX)) && a.range_flag) *a.range_flag = 1;
 }
 
+// Two consecutive units without pooling (2-3, 5-6, 8-9) as ONE kernel: the first unit's output y2
+// stays in registers (its residual role) and in LDS (BN + ReLU + split, as the second unit's staged
+// input), so it never reaches HBM, and the batch is staged from HBM once instead of twice.  All four
+// GEMMs run over the same NR rows i <-> global row rb + i (rb = block * RO - 4); each conv narrows the
+// rows it computes correctly by one at each end, so the second unit's output is right for i in
+// [4, NR - 4): RO = NR - 8 output rows per workgroup, every GEMM's tile row i is the same lane, and
+// y2 of row i is where the second unit's epilogue needs it.  LDS row L = i + 1 (rows 0 and NR + 1 are
+// zero pads, ZR the zero row of taps that leave a clip); one buffer, overwritten stage by stage.
+// FIN (units 8-9): the epilogue's AveragePooling1D(4) windows are 4 adjacent lanes (rb and RO are
+// multiples of 4), summed in the unfused kernel's order through DPP broadcasts.
+// Bit-identical to two siu launches: the same operands, MFMA sequences and epilogue arithmetic.
+template <int C, int NR, int NW, bool FIN, int MINW>
+__global__ void __launch_bounds__(64 * NW, MINW) siu_pair_kernel(SiuArgs a, SiuArgs b) {
+  constexpr int NT = 64 * NW;
+  constexpr int WN = C / 32;
+  constexpr int WM = NW / WN;
+  constexpr int MT = NR / (WM * 32);
+  constexpr int NCH = C / CK;
+  constexpr int LDP = C + 8;
+  constexpr int RO = NR - 8;
+  constexpr int ZR = NR + 2;
+  constexpr int QPP = CK / 4;
+  constexpr int MAXT = (NR * QPP + NT - 1) / NT;
+  static_assert(WM * WN == NW && MT * WM * 32 == NR && NT % QPP == 0 && RO % 4 == 0, "tiling");
+  __shared__ __attribute__((aligned(16))) _Float16 lhi[(NR + 3) * LDP];
+  __shared__ __attribute__((aligned(16))) _Float16 llo[(NR + 3) * LDP];
+  // per-channel parameters: unit a [0] b_a [1] 16 s_mid [2] 16 t_mid [3] b_b; unit b [4] 16 s_in
+  // [5] 16 t_in [6] b_a [7] 16 s_mid [8] 16 t_mid [9] b_b; FIN [10] fs [11] ft
+  __shared__ __attribute__((aligned(16))) float spar[12 * C];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave - (wave / WN) * WN;
+  const int HH = a.n * a.t;
+  const int rb = (int)blockIdx.x * RO - 4;
+  const int koff = (lane >> 5) * 8;
+  const int h4 = 4 * (lane >> 5);
+  const uint32_t tm = a.tdiv_m, ts = a.tdiv_s;
+  float rmax = 0.0f;
+  const __amdgpu_buffer_rsrc_t rx = siu_rsrc(a.x);
+
+  for (int e = tid; e < 3 * (LDP / 8); e += NT) {   // pad rows 0, NR + 1 and the zero row
+    const int z = e / (LDP / 8), k8 = e - z * (LDP / 8);
+    const int row = z == 0 ? 0 : z == 1 ? NR + 1 : ZR;
+    *reinterpret_cast<f16x8*>(lhi + row * LDP + 8 * k8) = f16x8{};
+    *reinterpret_cast<f16x8*>(llo + row * LDP + 8 * k8) = f16x8{};
+  }
+  for (int i = tid; i < C; i += NT) {
+    spar[i] = a.ba[i];
+    spar[C + i] = ACT_SCALE * a.s_mid[i];
+    spar[2 * C + i] = ACT_SCALE * a.t_mid[i];
+    spar[3 * C + i] = a.bb[i];
+    spar[4 * C + i] = ACT_SCALE * b.s_in[i];
+    spar[5 * C + i] = ACT_SCALE * b.t_in[i];
+    spar[6 * C + i] = b.ba[i];
+    spar[7 * C + i] = ACT_SCALE * b.s_mid[i];
+    spar[8 * C + i] = ACT_SCALE * b.t_mid[i];
+    spar[9 * C + i] = b.bb[i];
+    if constexpr (FIN) {
+      spar[10 * C + i] = b.fs[i];
+      spar[11 * C + i] = b.ft[i];
+    }
+  }
+
+  // ---- stage x rows i < NR (clamped to the batch: see siu_kernel) into LDS rows 1 .. NR ------------
+  {
+    const int q = tid % QPP;
+#pragma unroll 1
+    for (int ch = 0; ch < NCH; ++ch) {
+      const int ci = ch * CK + 4 * q;
+      float4 sc = *reinterpret_cast<const float4*>(a.s_in + ci);
+      float4 sh = *reinterpret_cast<const float4*>(a.t_in + ci);
+      sc = make_float4(ACT_SCALE * sc.x, ACT_SCALE * sc.y, ACT_SCALE * sc.z, ACT_SCALE * sc.w);
+      sh = make_float4(ACT_SCALE * sh.x, ACT_SCALE * sh.y, ACT_SCALE * sh.z, ACT_SCALE * sh.w);
+      float4 pre[MAXT];
+#pragma unroll
+      for (int j = 0; j < MAXT; ++j) {
+        const int task = tid + j * NT;
+        const int g = min(max(rb + task / QPP, 0), HH - 1);
+        pre[j] = ld4(rx, (uint32_t)g * (C * 4u) + ci * 4u);
+      }
+#pragma unroll
+      for (int j = 0; j < MAXT; ++j) {
+        const int task = tid + j * NT;
+        if (MAXT * NT > NR * QPP && task >= NR * QPP) continue;
+        f16x4 hv, lv;
+        bn_split4(pre[j], sc, sh, hv, lv, rmax);
+        const int row = task / QPP + 1;
+        *reinterpret_cast<f16x4*>(lhi + row * LDP + ci) = hv;
+        *reinterpret_cast<f16x4*>(llo + row * LDP + ci) = lv;
+      }
+    }
+  }
+
+  constexpr int kstride = (C / 32) * 512;
+  constexpr int tap_stride = C * NCH * CK;
+  const int lofs = wn * 512 + lane * 8;
+  int mrow[MT], trow[MT], grow[MT];   // per tile: this lane's row i, its position in its clip, rb + i
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    mrow[mt] = (wm * MT + mt) * 32 + (lane & 31);
+    grow[mt] = rb + mrow[mt];
+    const uint32_t gp = (uint32_t)(grow[mt] + a.t);
+    trow[mt] = (int)(gp - tdiv(gp, tm, ts) * (uint32_t)a.t);
+  }
+  // acc = W^T X^T over LDS rows (row i's taps: LDS rows i .. i + 2, or the zero row)
+  auto gemm = [&](const uint16_t* wh, const uint16_t* wl, f32x16 (&acc)[MT]) {
+    const __amdgpu_buffer_rsrc_t rwh = siu_rsrc(wh), rwl = siu_rsrc(wl);
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[mt][i] = 0.0f;
+#pragma unroll 1
+    for (int ch = 0; ch < NCH; ++ch) {
+#pragma unroll 1
+      for (int tap = 0; tap < TAPS; ++tap) {
+        f16x8 bh[KS], bl[KS];
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+          const int u = tap * tap_stride + (ch * KS + s) * kstride;
+          bh[s] = ldw(rwh, lofs, u);
+          bl[s] = ldw(rwl, lofs, u);
+        }
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt) {
+            const int src = trow[mt] + tap - 1;
+            const int off = (src < 0 || src >= a.t ? ZR : mrow[mt] + tap) * LDP + ch * CK + 16 * s + koff;
+            const f16x8 ah = *reinterpret_cast<const f16x8*>(lhi + off);
+            const f16x8 al = *reinterpret_cast<const f16x8*>(llo + off);
+            acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(bl[s], ah, acc[mt], 0, 0, 0);
+            acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(bh[s], al, acc[mt], 0, 0, 0);
+            acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(bh[s], ah, acc[mt], 0, 0, 0);
+          }
+      }
+    }
+  };
+  // LDS row i + 1 = split(max(fma(v, s16, t16), 0)) of each tile's row, v = fma(acc, u, bias) or the
+  // values themselves (P < 0); rows outside [lo, NR - lo) or the batch stay out of the range guard
+  auto put = [&](const float (&v)[MT][16], int ps, int pt, int lo) {
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const int L = mrow[mt] + 1;
+      float tmax = 0.0f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int co0 = wn * 32 + 8 * q + h4;
+        const float4 s = *reinterpret_cast<const float4*>(spar + ps * C + co0);
+        const float4 t = *reinterpret_cast<const float4*>(spar + pt * C + co0);
+        f16x4 hv, lv;
+        bn_split4(make_float4(v[mt][4 * q], v[mt][4 * q + 1], v[mt][4 * q + 2], v[mt][4 * q + 3]), s, t, hv, lv,
+                  tmax);
+        *reinterpret_cast<f16x4*>(lhi + L * LDP + co0) = hv;
+        *reinterpret_cast<f16x4*>(llo + L * LDP + co0) = lv;
+      }
+      if (mrow[mt] >= lo && mrow[mt] < NR - lo && grow[mt] >= 0 && grow[mt] < HH) rmax = fmaxf(rmax, tmax);
+    }
+  };
+  // v = fma(acc, u, bias[pb]) (+ r)
+  auto unscale = [&](const f32x16 (&acc)[MT], float u, int pb, float (&v)[MT][16]) {
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 bq = *reinterpret_cast<const float4*>(spar + pb * C + wn * 32 + 8 * q + h4);
+        v[mt][4 * q] = fmaf(acc[mt][4 * q], u, bq.x);
+        v[mt][4 * q + 1] = fmaf(acc[mt][4 * q + 1], u, bq.y);
+        v[mt][4 * q + 2] = fmaf(acc[mt][4 * q + 2], u, bq.z);
+        v[mt][4 * q + 3] = fmaf(acc[mt][4 * q + 3], u, bq.w);
+      }
+  };
+
+  f32x16 acc[MT];
+  float v[MT][16];
+  __syncthreads();
+  // unit a: t1 (rows 1 .. NR - 2 right)
+  gemm(a.wah, a.wal, acc);
+  __syncthreads();
+  unscale(acc, a.ua, 0, v);
+  put(v, 1, 2, 1);
+  // y2 = x + conv_b (rows 2 .. NR - 3 right): the raw x of each tile row, loaded under GEMM b
+  float y2[MT][16];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int g = min(max(grow[mt], 0), HH - 1);
+      const float4 r = ld4(rx, (uint32_t)g * (C * 4u) + (wn * 32 + 8 * q + h4) * 4u);
+      y2[mt][4 * q] = r.x;
+      y2[mt][4 * q + 1] = r.y;
+      y2[mt][4 * q + 2] = r.z;
+      y2[mt][4 * q + 3] = r.w;
+    }
+  __syncthreads();
+  gemm(a.wbh, a.wbl, acc);
+  unscale(acc, a.ub, 3, v);
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) y2[mt][r] = v[mt][r] + y2[mt][r];
+  __syncthreads();   // every wave has read t1
+  // unit b: its staged input, then t1 (rows 3 .. NR - 4 right), then the output (rows 4 .. NR - 5)
+  put(y2, 4, 5, 2);
+  __syncthreads();
+  gemm(b.wah, b.wal, acc);
+  __syncthreads();
+  unscale(acc, b.ua, 6, v);
+  put(v, 7, 8, 3);
+  __syncthreads();
+  gemm(b.wbh, b.wbl, acc);
+  unscale(acc, b.ub, 9, v);
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    const int i = mrow[mt], g = grow[mt];
+    const bool ok = i >= 4 && i < NR - 4 && g < HH;
+    if constexpr (!FIN) {
+      if (ok) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float4 val = make_float4(v[mt][4 * q] + y2[mt][4 * q], v[mt][4 * q + 1] + y2[mt][4 * q + 1],
+                                         v[mt][4 * q + 2] + y2[mt][4 * q + 2], v[mt][4 * q + 3] + y2[mt][4 * q + 3]);
+          *reinterpret_cast<float4*>(b.y + (size_t)g * C + wn * 32 + 8 * q + h4) = val;
+        }
+      }
+    } else {
+      // BN + ReLU of each row, then the 4-row window sum in the unfused order ((r0 + r1) + r2) + r3:
+      // lanes 4k .. 4k + 3 hold rows rb + i, i = 0 .. 3 mod 4
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int co0 = wn * 32 + 8 * q + h4;
+        const float4 fs = *reinterpret_cast<const float4*>(spar + 10 * C + co0);
+        const float4 ft = *reinterpret_cast<const float4*>(spar + 11 * C + co0);
+        const float fsv[4] = {fs.x, fs.y, fs.z, fs.w}, ftv[4] = {ft.x, ft.y, ft.z, ft.w};
+        float out[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float val = v[mt][4 * q + e] + y2[mt][4 * q + e];
+          const int r = __builtin_bit_cast(int, fmaxf(fmaf(val, fsv[e], ftv[e]), 0.0f));
+          const float r0 = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(r, 0x00, 0xf, 0xf, false));
+          const float r1 = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(r, 0x55, 0xf, 0xf, false));
+          const float r2 = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(r, 0xaa, 0xf, 0xf, false));
+          const float r3 = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(r, 0xff, 0xf, 0xf, false));
+          out[e] = (((r0 + r1) + r2) + r3) / 4.0f;
+        }
+        if (ok && (i & 3) == 0)
+          *reinterpret_cast<float4*>(b.seq + (size_t)(g >> 2) * C + co0) = make_float4(out[0], out[1], out[2], out[3]);
+      }
+    }
+  }
+  if (!(rmax < SPLIT_MAX) && a.range_flag) *a.range_flag = 1;
+}
+
 // q = x / d for x < 2^31 as (umulhi(x, m) + x) >> s: s = ceil(log2 d), m = floor(2^(32+s) / d) + 1 - 2^32
 void siu_fastdiv(uint32_t d, uint32_t& m, uint32_t& s) {
   s = 0;
@@ -384,7 +636,35 @@ hipError_t launch(const SiuArgs& a0, hipStream_t s) {
   return hipGetLastError();
 }
 
+template <int C, int NR, int NW, bool FIN, int MINW>
+hipError_t launch_pair(const SiuArgs& a0, const SiuArgs& b, hipStream_t s) {
+  constexpr int RO = NR - 8;
+  SiuArgs a = a0;
+  siu_fastdiv((uint32_t)a.t, a.tdiv_m, a.tdiv_s);
+  const int64_t rows = (int64_t)a.n * a.t;
+  if (rows >= (1 << 24) || rows * C * 4 > 0xffffff00ll) return hipErrorInvalidValue;
+  const int64_t blocks = (rows + RO - 1) / RO;
+  hipLaunchKernelGGL((siu_pair_kernel<C, NR, NW, FIN, MINW>), dim3((unsigned)blocks), dim3(64 * NW), 0, s, a, b);
+  return hipGetLastError();
+}
+
 }  // namespace
+
+bool siu_pair_supported(int c) { return c == 32 || c == 64 || c == 128; }
+
+hipError_t siu_pair_launch(const SiuArgs& a, const SiuArgs& b, int c, hipStream_t s) {
+  if ((int64_t)a.n * a.t == 0) return hipSuccess;
+  if (!a.x || a.n != b.n || a.t != b.t || a.t < 1) return hipErrorInvalidValue;
+  if (b.seq) {   // units 8-9 with the final BN + ReLU + AveragePooling1D(4)
+    if (!b.fs || !b.ft || a.t % 4 != 0 || c != 128) return hipErrorInvalidValue;
+    return launch_pair<128, 128, 4, true, 2>(a, b, s);
+  }
+  if (!b.y || b.y == a.x) return hipErrorInvalidValue;
+  if (c == 32) return launch_pair<32, 256, 4, false, 3>(a, b, s);
+  if (c == 64) return launch_pair<64, 256, 4, false, 2>(a, b, s);
+  if (c == 128) return launch_pair<128, 128, 4, false, 2>(a, b, s);
+  return hipErrorInvalidValue;
+}
 
 bool siu_supported(int c) { return c == 32 || c == 64 || c == 128; }
 

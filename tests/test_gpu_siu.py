@@ -4,7 +4,9 @@ probabilities over a batch with ragged and 'silent' clips, across several tiles 
 * MMLA_NO_SIU: units without pooling (Conv1D -> BN -> ReLU -> Conv1D + residual, t1 kept in LDS);
 * MMLA_NO_SIPU: the pool units (MaxPool1D in the staging, the stride-2 shortcut in the epilogue);
 * MMLA_NO_SIFIN: the last unit writing the final BN + ReLU + AveragePooling1D(4) itself;
-* MMLA_NO_SIPAD: si_fe's 40-float feature rows (zero 40th column) read by the stem as float4.
+* MMLA_NO_SIPAD: si_fe's 40-float feature rows (zero 40th column) read by the stem as float4;
+* MMLA_NO_SIPAIR: two consecutive units without pooling as one kernel (the first unit's output kept
+  on chip), with and without the last unit's fused pooling.
 Each switch is set explicitly, so the tests hold whatever the library's defaults are."""
 import numpy as np
 import pytest
@@ -13,8 +15,10 @@ from oracle import synth
 
 pytestmark = pytest.mark.gpu
 
-ALL_ON = {'MMLA_NO_SIU': '0', 'MMLA_NO_SIPU': '0', 'MMLA_NO_SIFIN': '0', 'MMLA_NO_SIPAD': '0'}
-ALL_OFF = {'MMLA_NO_SIU': '1', 'MMLA_NO_SIPU': '1', 'MMLA_NO_SIFIN': '1', 'MMLA_NO_SIPAD': '1'}
+ALL_ON = {'MMLA_NO_SIU': '0', 'MMLA_NO_SIPU': '0', 'MMLA_NO_SIFIN': '0', 'MMLA_NO_SIPAD': '0',
+          'MMLA_NO_SIPAIR': '0'}
+ALL_OFF = {'MMLA_NO_SIU': '1', 'MMLA_NO_SIPU': '1', 'MMLA_NO_SIFIN': '1', 'MMLA_NO_SIPAD': '1',
+           'MMLA_NO_SIPAIR': '1'}
 
 
 def _ctx(monkeypatch, env):
@@ -56,3 +60,14 @@ def test_fused_final_pool_bit_identical(monkeypatch, pcm):
 
 def test_padded_feature_rows_bit_identical(monkeypatch, pcm):
     _same(monkeypatch, pcm, ALL_ON, dict(ALL_ON, MMLA_NO_SIPAD='1'))
+
+
+def test_unit_pairs_bit_identical(monkeypatch, pcm):
+    _same(monkeypatch, pcm, ALL_ON, dict(ALL_ON, MMLA_NO_SIPAIR='1'))
+    _same(monkeypatch, pcm, dict(ALL_ON, MMLA_NO_SIFIN='1'), dict(ALL_ON, MMLA_NO_SIPAIR='1', MMLA_NO_SIFIN='1'))
+
+
+@pytest.mark.parametrize('n', [1, 2, 5])
+def test_unit_pairs_small_batches(monkeypatch, pcm, n):
+    """batches smaller than one pair workgroup's rows (every row clamped at both batch ends)"""
+    _same(monkeypatch, pcm[:n], ALL_ON, ALL_OFF)
