@@ -111,6 +111,7 @@ struct SG {
   static constexpr int PD = CIN == 16 ? 1 : 2;                      // input prefetch distance (chunks)
   static_assert(H % R == 0, "geometry");
   static_assert(NT % QPP == 0, "a thread's channel quad is fixed");
+  static_assert(XROW <= 1024 && W * CIN * 4 < 65536 && W * 12 < 65536, "staging task fields");
 };
 
 // the x ring: pixel (row r, halo column x), 16-B channel group g -> half offset in a plane
@@ -219,7 +220,8 @@ __global__ void __launch_bounds__(NT, (SG<H, W, CIN, POOL>::MINB)) rbs_kernel(Re
       __builtin_amdgcn_make_buffer_rsrc(im8 ? (void*)(a.img8 + (int64_t)clip * H * W * 3)
                                             : (void*)(a.imgf + (int64_t)clip * H * W * 3),
                                         (short)0, (int)(H * W * 3 * (im8 ? 1 : 4)), 0x00020000);
-  // per task: LDS column offset (bits 0-13), tile row (14-17), column inside the image (18), task exists (19)
+  // per task: LDS column offset (bits 0-9), tile row (10-13), column inside the image (14), task exists
+  // (15), its source byte offset within a row (16-31)
   uint32_t tinfo[G::MAXT];
 #pragma unroll
   for (int j = 0; j < G::MAXT; ++j) {
@@ -227,10 +229,11 @@ __global__ void __launch_bounds__(NT, (SG<H, W, CIN, POOL>::MINB)) rbs_kernel(Re
     const int px = t / G::QPP;
     const int rr = px / G::XW, x = px - rr * G::XW;
     const int iw = w0 - 1 + x;
-    tinfo[j] = (uint32_t)(xoff<CIN>(0, x, q >> 1) + 4 * (q & 1)) | ((uint32_t)(rr & 15) << 14) |
-               ((uint32_t)(iw >= 0 && iw < W) << 18) | ((uint32_t)(rr < R) << 19);
+    const bool col_ok = iw >= 0 && iw < W;
+    const uint32_t tc = !col_ok ? 0u : STEM ? (uint32_t)iw * (a.img8 ? 3u : 12u) : (uint32_t)(iw * CIN + 4 * q) * 4u;
+    tinfo[j] = (uint32_t)(xoff<CIN>(0, x, q >> 1) + 4 * (q & 1)) | ((uint32_t)(rr & 15) << 10) |
+               ((uint32_t)col_ok << 14) | ((uint32_t)(rr < R) << 15) | (tc << 16);
   }
-  auto task_col = [&](int j) { return w0 - 1 + ((tid + j * NT) / G::QPP) % G::XW; };
   // the image pixel {r, g, b, 1} (1: inside the image), or x channels 4q .. 4q+3
   // (no branch around a load: a load inside a divergent branch is waited for inside it; the raw image
   // bytes are converted where they are used)
@@ -261,9 +264,25 @@ __global__ void __launch_bounds__(NT, (SG<H, W, CIN, POOL>::MINB)) rbs_kernel(Re
                          (float)__builtin_bit_cast(uint32_t, v.z), 0.f);
     return v;
   };
+  // task j's 4 channels at x row r0 + its tile row (rows outside the image: the wrapped or past-the-end
+  // row offset is out of range, as in load_src)
   auto load_task = [&](int r0, int j) -> float4 {
     const uint32_t ti = tinfo[j];
-    return load_src(r0 + (int)((ti >> 14) & 15), task_col(j), (ti >> 18) & 1);
+    const uint32_t off = (ti >> 14) & 1u ? (uint32_t)((r0 + (int)((ti >> 10) & 15)) * (STEM ? W * 3 * (im8 ? 1 : 4) : (int)ROWB)) + (ti >> 16)
+                                         : 0x80000000u;
+    if constexpr (STEM) {
+      if (im8) {
+        const uint32_t r = __builtin_amdgcn_raw_buffer_load_b8(rimg, off, 0, 0);
+        const uint32_t g = __builtin_amdgcn_raw_buffer_load_b8(rimg, off + 1u, 0, 0);
+        const uint32_t b = __builtin_amdgcn_raw_buffer_load_b8(rimg, off + 2u, 0, 0);
+        return make_float4(__builtin_bit_cast(float, r), __builtin_bit_cast(float, g), __builtin_bit_cast(float, b), 0.f);
+      }
+      return make_float4(__builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rimg, off, 0, 0)),
+                         __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rimg, off + 4u, 0, 0)),
+                         __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rimg, off + 8u, 0, 0)), 0.f);
+    } else {
+      return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rx, off, 0, 0));
+    }
   };
   // BN1 + ELU (+ the stem) + split of one task's 4 channels at x row ih, into the x ring at lds
   // BN1 + ELU (+ the stem) + split of one task's 4 channels into the x ring at half offset o; MASK:
@@ -296,11 +315,11 @@ __global__ void __launch_bounds__(NT, (SG<H, W, CIN, POOL>::MINB)) rbs_kernel(Re
   // column stays zero); rows past the image only occur in the last chunk (MASK)
   auto stage_task = [&](int r0, int j, float4 v, auto MASK_) {
     const uint32_t ti = tinfo[j];
-    if ((ti >> 18) != 3u) return;   // task exists and its column is inside the image
-    const int rr = (int)((ti >> 14) & 15);
+    if (((ti >> 14) & 3u) != 3u) return;   // task exists and its column is inside the image
+    const int rr = (int)((ti >> 10) & 15);
     uint32_t slot = (uint32_t)((r0 + 1) % G::XRING) + (uint32_t)rr;   // (r0 + 1) % XRING: scalar
     slot = min(slot, slot - (uint32_t)G::XRING);
-    stage4((int)slot * G::XROW + (int)(ti & 16383), r0 + rr < H, v, MASK_);
+    stage4((int)slot * G::XROW + (int)(ti & 1023), r0 + rr < H, v, MASK_);
   };
   // the ring's columns outside the image (strip 0: image column -1; the last strip: columns >= W),
   // zeroed once in every slot and both planes: no task writes them
@@ -335,7 +354,10 @@ __global__ void __launch_bounds__(NT, (SG<H, W, CIN, POOL>::MINB)) rbs_kernel(Re
     for (int i = 0; i < 16; ++i) acc[i] = 0.0f;
     int xr[3];
 #pragma unroll
-    for (int dy = 0; dy < 3; ++dy) xr[dy] = ((j0 + nr + dy) % G::XRING) * G::XROW;   // x row j - 1 + dy
+    for (int dy = 0; dy < 3; ++dy) {   // x row j - 1 + dy: ring slot (j0 % XRING: scalar) + nr + dy, wrapped
+      const uint32_t sl = (uint32_t)(j0 % G::XRING) + (uint32_t)(nr + dy);
+      xr[dy] = (int)min(sl, sl - (uint32_t)G::XRING) * G::XROW;
+    }
     // the x fragments one k-step ahead (an LDS read's latency would otherwise sit before every
     // step's MFMAs)
     auto xo = [&](int s) {
@@ -367,7 +389,8 @@ __global__ void __launch_bounds__(NT, (SG<H, W, CIN, POOL>::MINB)) rbs_kernel(Re
   // zero padding (j0 is even and so is H: both rows of a wave are inside or both outside)
   auto t1_write = [&](int j0, const f32x16& acc) {
     const int j = j0 + nr;
-    const int slot = (j + 1) % G::TRING;
+    const uint32_t sl = (uint32_t)((j0 + 1) % G::TRING) + (uint32_t)nr;   // (j + 1) % TRING
+    const int slot = (int)min(sl, sl - (uint32_t)G::TRING);
     if (j0 < H) {
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj) {
@@ -490,7 +513,8 @@ __global__ void __launch_bounds__(NT, (SG<H, W, CIN, POOL>::MINB)) rbs_kernel(Re
 #pragma unroll
       for (int dy = 0; dy < 4; ++dy) {
         tj[dy] = o0 + pr - 1 + dy;
-        tr[dy] = (tj[dy] + 1) % G::TRING;
+        const uint32_t sl = (uint32_t)(o0 % G::TRING) + (uint32_t)(pr + dy);   // (tj + 1) % TRING
+        tr[dy] = (int)min(sl, sl - (uint32_t)G::TRING);
       }
       auto to = [&](int s) { return toff<POOL>(tr[s >> 1], tj[s >> 1], pc, 2 * (s & 1) + h); };
       f16x8 nxh = *reinterpret_cast<const f16x8*>(st + to(0));
