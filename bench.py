@@ -140,9 +140,10 @@ def rank_devices(world, rank, local):
     return out
 
 
-def roofline(prof, wl, clips_per_launch, prec):
-    """dominant stage: algorithmic work per launch / average launch time (HIP events)"""
-    stage = max(prof, key=lambda s: prof[s][0])
+def roofline(prof, wl, clips_per_launch, prec, stage=None):
+    """dominant stage (or `stage`): algorithmic work per launch / average launch time (HIP events)"""
+    if stage is None:
+        stage = max(prof, key=lambda s: prof[s][0])
     ms, launches, work = prof[stage]
     if stage in HBM_STAGES:
         achieved = work / (ms * 1e-3) / 1e9
@@ -374,6 +375,10 @@ def main():
     dt, prof = timed(args.steps, args.warmup)
     value = world * clips * args.steps / dt
     roof = roofline(prof, wl, mb, PREC_F16X3)
+    # the convolution stack's own roofline when another stage dominates the step (the SI pipeline since
+    # round 6: its float64 front-end takes longer than the fused res-unit chains)
+    roof_conv = (roofline(prof, wl, mb, PREC_F16X3, 'conv')
+                 if roof['kernel'] != 'conv' and prof.get('conv', (0, 0, 0))[1] else None)
     stages = stage_table(prof)
     range_ok = True
     try:
@@ -482,7 +487,7 @@ def main():
                        'global_batch': world * clips, 'clip_samples': clip_len, 'microbatch': mb,
                        'parallelism': f'dp{world}' + ('+rccl_allgather_logits' if world > 1 and pipeline else '')},
             'world_size': world, 'gpus_requested': args.gpus, 'rank_devices': devices,
-            'roofline': roof, 'stages': stages, 'fe': fe, 'precision_f32': f32,
+            'roofline': roof, 'roofline_conv': roof_conv, 'stages': stages, 'fe': fe, 'precision_f32': f32,
             'range_guard_ok': range_ok, 'cpu_baseline': cpu, 'parity': parity,
             'latency': latency,
         }

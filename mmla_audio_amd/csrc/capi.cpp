@@ -138,6 +138,9 @@ struct mmla_ctx {
   // ... and two consecutive units without pooling (2-3, 5-6, 8-9) as one kernel (siu.hip
   // siu_pair_kernel: the first unit's output stays on chip); env MMLA_NO_SIPAIR=1: one launch each
   bool sipair = true;
+  // ... and a pool unit with the two units after it (1-3, 4-6, 7-9) as one kernel (siu.hip
+  // siu_chain_kernel POOL); env MMLA_NO_SICHAIN=1: the pool unit alone, then the pair
+  bool sichain = true;
   // fused SI pipeline: si_fe writes 40-float feature rows for the stem (env MMLA_NO_SIPAD=1: 39)
   bool si_pad_feat = true;
   // OD blocks 4-9 as one fused kernel each (odu.hip: t1 on chip); env MMLA_NO_ODU=1 at create: the
@@ -1187,9 +1190,27 @@ int run_si_net(mmla_ctx* c, const float* x, int64_t n, float* probs, int32_t* ar
       s.bs = U.sc.bias;
       s.us = U.sc.unscale();
       s.range_flag = c->range_ptr;
-      const double C = U.ca.cout;
-      LAUNCH(c, MMLA_STAGE_CONV, 2.0 * n * tp * (3.0 * cin * C + 3.0 * C * C + cin * C),
-             sipu_launch(s, cin, U.ca.cout, c->stream));
+      const int C = U.ca.cout;
+      const double pool_flops = 2.0 * n * tp * (3.0 * cin * C + 3.0 * C * C + cin * C);
+      // ... with the two units after it (siu.hip chain: both intermediates stay on chip)
+      if (c->sichain && u + 2 < 9 && !POOL[u + 1] && !POOL[u + 2] && siu_triple_supported(cin, C) &&
+          siu_ok(W.unit[u + 1], C) && siu_ok(W.unit[u + 2], C)) {
+        SiuArgs sa = siu_args(W.unit[u + 1], nullptr, nullptr, n, tp, c->range_ptr);
+        SiuArgs sb = siu_args(W.unit[u + 2], nullptr, R, n, tp, c->range_ptr);
+        if (u + 2 == 8 && c->sifin && siu_final_supported(C) && tp % 4 == 0) {
+          sb.y = nullptr;
+          sb.seq = static_cast<float*>(pseq);
+          sb.fs = W.final_bn.scale;
+          sb.ft = W.final_bn.shift;
+          fused_final = true;
+        }
+        s.y = nullptr;
+        LAUNCH(c, MMLA_STAGE_CONV, pool_flops + 2.0 * 2.0 * 2.0 * n * tp * 3 * C * C,
+               siu_triple_launch(s, sa, sb, cin, C, c->stream));
+        u += 2;
+      } else {
+        LAUNCH(c, MMLA_STAGE_CONV, pool_flops, sipu_launch(s, cin, U.ca.cout, c->stream));
+      }
       std::swap(X, R);
       t = tp;
     } else if (POOL[u]) {
@@ -1402,6 +1423,7 @@ int mmla_create(int device, mmla_ctx** out) {
   if (const char* sp = std::getenv("MMLA_NO_SIPU")) c->sipu = std::atoi(sp) == 0;
   if (const char* sf = std::getenv("MMLA_NO_SIFIN")) c->sifin = std::atoi(sf) == 0;
   if (const char* sq = std::getenv("MMLA_NO_SIPAIR")) c->sipair = std::atoi(sq) == 0;
+  if (const char* sc = std::getenv("MMLA_NO_SICHAIN")) c->sichain = std::atoi(sc) == 0;
   if (const char* ls = std::getenv("MMLA_NO_LSTM_SPLIT")) c->lstm_split = std::atoi(ls) == 0;
   if (const char* lm = std::getenv("MMLA_LSTM_SPLIT_MAX")) c->lstm_split_max = std::atoi(lm);
   if (const char* sp = std::getenv("MMLA_DEBUG_LSTM_SPIN")) c->lstm_spin = std::atoi(sp);

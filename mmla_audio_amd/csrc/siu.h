@@ -40,6 +40,11 @@ hipError_t siu_launch(const SiuArgs& a, int c, hipStream_t stream);
 // b.seq set: b is the last unit (siu_final_supported's epilogue)
 bool siu_pair_supported(int c);
 hipError_t siu_pair_launch(const SiuArgs& a, const SiuArgs& b, int c, hipStream_t stream);
+// a pool unit p and the two units after it (p.x the input, b.y / b.seq the output: the
+// intermediates stay on chip)
+bool siu_triple_supported(int cin, int c);
+hipError_t siu_triple_launch(const SiuArgs& p, const SiuArgs& a, const SiuArgs& b, int cin, int c,
+                             hipStream_t stream);
 // the pool unit (speaker_identification.py:170-172 + 173-188) with t1 kept on chip
 bool sipu_supported(int cin, int c);
 hipError_t sipu_launch(const SiuArgs& a, int cin, int c, hipStream_t stream);

@@ -363,45 +363,60 @@ __global__ void __launch_bounds__(64 * NW, MINW) siu_kernel(SiuArgs a) {
   if ((rbad || !(rmax < SPLIT_MAX)) && a.range_flag) *a.range_flag = 1;
 }
 
-// Two consecutive units without pooling (2-3, 5-6, 8-9) as ONE kernel: the first unit's output y2
-// stays in registers (its residual role) and in LDS (BN + ReLU + split, as the second unit's staged
-// input), so it never reaches HBM, and the batch is staged from HBM once instead of twice.  All four
-// GEMMs run over the same NR rows i <-> global row rb + i (rb = block * RO - 4); each conv narrows the
-// rows it computes correctly by one at each end, so the second unit's output is right for i in
-// [4, NR - 4): RO = NR - 8 output rows per workgroup, every GEMM's tile row i is the same lane, and
-// y2 of row i is where the second unit's epilogue needs it.  LDS row L = i + 1 (rows 0 and NR + 1 are
-// zero pads, ZR the zero row of taps that leave a clip); one buffer, overwritten stage by stage.
-// FIN (units 8-9): the epilogue's AveragePooling1D(4) windows are 4 adjacent lanes (rb and RO are
-// multiples of 4), summed in the unfused kernel's order through DPP broadcasts.
-// Bit-identical to two siu launches: the same operands, MFMA sequences and epilogue arithmetic.
-template <int C, int NR, int NW, bool FIN, int MINW>
-__global__ void __launch_bounds__(64 * NW, MINW) siu_pair_kernel(SiuArgs a, SiuArgs b) {
+// the chain kernel's first output row per workgroup (its halo in front) and output rows: U units
+// narrow the correct rows by 2 U; FIN keeps both multiples of 4 (pool windows)
+template <bool POOL, bool FIN>
+constexpr int chain_front() { return POOL ? (FIN ? 8 : 6) : 4; }
+template <int NR, bool POOL, bool FIN>
+constexpr int chain_rows() { return FIN ? (NR - chain_front<POOL, FIN>() - (POOL ? 6 : 4)) / 4 * 4 : NR - (POOL ? 12 : 8); }
+
+// A chain of res units as ONE kernel: two consecutive units without pooling (2-3, 5-6, 8-9), or with
+// POOL the pool unit before them too (1-3, 4-6, 7-9).  Each unit's output stays in registers (the next
+// unit's residual) and in LDS (BN + ReLU + split, the next unit's staged input), so only the chain's
+// input and output touch HBM.  All GEMMs run over the same NR rows i <-> global (pooled) row rb + i;
+// each conv narrows the rows it computes correctly by one at each end, so the last unit's output is
+// right for i in [2 U, NR - 2 U), U = the chain's units: every GEMM's tile row i is the same lane,
+// and the running residual of row i is where the next epilogue needs it.  Output rows per workgroup
+// RO = [F, F + RO), F = 2 U (FIN: 8 with POOL, so that rb and RO are multiples of 4).  LDS row
+// L = i + 1 (rows 0 and NR + 1 are zero pads, ZR the zero row of taps that leave a clip); one buffer,
+// overwritten stage by stage.  FIN (unit 9 last): the AveragePooling1D(4) windows are 4 adjacent
+// lanes, summed in the unfused kernel's order through DPP broadcasts.
+// Bit-identical to one siu launch per unit: the same operands, MFMA sequences and epilogue arithmetic.
+template <int CIN, int C, int NR, int NW, bool POOL, bool FIN, int MINW>
+__global__ void __launch_bounds__(64 * NW, MINW) siu_chain_kernel(SiuArgs p, SiuArgs a, SiuArgs b) {
   constexpr int NT = 64 * NW;
   constexpr int WN = C / 32;
   constexpr int WM = NW / WN;
   constexpr int MT = NR / (WM * 32);
-  constexpr int NCH = C / CK;
+  constexpr int NCHX = CIN / CK, NCH = C / CK;
   constexpr int LDP = C + 8;
-  constexpr int RO = NR - 8;
+  constexpr int F = chain_front<POOL, FIN>(), RO = chain_rows<NR, POOL, FIN>();
   constexpr int ZR = NR + 2;
   constexpr int QPP = CK / 4;
   constexpr int MAXT = (NR * QPP + NT - 1) / NT;
-  static_assert(WM * WN == NW && MT * WM * 32 == NR && NT % QPP == 0 && RO % 4 == 0, "tiling");
+  constexpr int P0 = POOL ? 2 : 0;     // rows the pool unit narrows
+  static_assert(WM * WN == NW && MT * WM * 32 == NR && NT % QPP == 0, "tiling");
+  static_assert(POOL || CIN == C, "units without pooling keep their width");
+  static_assert(F + RO <= NR - (POOL ? 6 : 4) && (!FIN || (F % 4 == 0 && RO % 4 == 0)), "rows");
   __shared__ __attribute__((aligned(16))) _Float16 lhi[(NR + 3) * LDP];
   __shared__ __attribute__((aligned(16))) _Float16 llo[(NR + 3) * LDP];
   // per-channel parameters: unit a [0] b_a [1] 16 s_mid [2] 16 t_mid [3] b_b; unit b [4] 16 s_in
-  // [5] 16 t_in [6] b_a [7] 16 s_mid [8] 16 t_mid [9] b_b; FIN [10] fs [11] ft
-  __shared__ __attribute__((aligned(16))) float spar[12 * C];
+  // [5] 16 t_in [6] b_a [7] 16 s_mid [8] 16 t_mid [9] b_b; FIN [10] fs [11] ft; POOL: unit a [12]
+  // 16 s_in [13] 16 t_in, the pool unit [14] b_a [15] 16 s_mid [16] 16 t_mid [17] b_b [18] b_s
+  constexpr int NPAR = POOL ? 19 : 12;
+  __shared__ __attribute__((aligned(16))) float spar[NPAR * C];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave - (wave / WN) * WN;
+  const SiuArgs& s0 = POOL ? p : a;                // the chain's first unit
   const int HH = a.n * a.t;
-  const int rb = (int)blockIdx.x * RO - 4;
+  const int rb = (int)blockIdx.x * RO - F;
   const int koff = (lane >> 5) * 8;
   const int h4 = 4 * (lane >> 5);
   const uint32_t tm = a.tdiv_m, ts = a.tdiv_s;
   float rmax = 0.0f;
-  const __amdgpu_buffer_rsrc_t rx = siu_rsrc(a.x);
+  int rbad = 0;   // a raw shortcut operand out of range / NaN (an int, pinned per tile: see below)
+  const __amdgpu_buffer_rsrc_t rx = siu_rsrc(s0.x);
 
   for (int e = tid; e < 3 * (LDP / 8); e += NT) {   // pad rows 0, NR + 1 and the zero row
     const int z = e / (LDP / 8), k8 = e - z * (LDP / 8);
@@ -424,16 +439,26 @@ __global__ void __launch_bounds__(64 * NW, MINW) siu_pair_kernel(SiuArgs a, SiuA
       spar[10 * C + i] = b.fs[i];
       spar[11 * C + i] = b.ft[i];
     }
+    if constexpr (POOL) {
+      spar[12 * C + i] = ACT_SCALE * a.s_in[i];
+      spar[13 * C + i] = ACT_SCALE * a.t_in[i];
+      spar[14 * C + i] = p.ba[i];
+      spar[15 * C + i] = ACT_SCALE * p.s_mid[i];
+      spar[16 * C + i] = ACT_SCALE * p.t_mid[i];
+      spar[17 * C + i] = p.bb[i];
+      spar[18 * C + i] = p.bs[i];
+    }
   }
 
-  // ---- stage x rows i < NR (clamped to the batch: see siu_kernel) into LDS rows 1 .. NR ------------
+  // ---- stage the chain's input rows i < NR (clamped to the batch: see siu_kernel; POOL: row g =
+  //      (clip, tt) is the max of the clip's unpooled rows 2 tt, 2 tt + 1) into LDS rows 1 .. NR ------
   {
     const int q = tid % QPP;
 #pragma unroll 1
-    for (int ch = 0; ch < NCH; ++ch) {
+    for (int ch = 0; ch < NCHX; ++ch) {
       const int ci = ch * CK + 4 * q;
-      float4 sc = *reinterpret_cast<const float4*>(a.s_in + ci);
-      float4 sh = *reinterpret_cast<const float4*>(a.t_in + ci);
+      float4 sc = *reinterpret_cast<const float4*>(s0.s_in + ci);
+      float4 sh = *reinterpret_cast<const float4*>(s0.t_in + ci);
       sc = make_float4(ACT_SCALE * sc.x, ACT_SCALE * sc.y, ACT_SCALE * sc.z, ACT_SCALE * sc.w);
       sh = make_float4(ACT_SCALE * sh.x, ACT_SCALE * sh.y, ACT_SCALE * sh.z, ACT_SCALE * sh.w);
       float4 pre[MAXT];
@@ -441,7 +466,16 @@ __global__ void __launch_bounds__(64 * NW, MINW) siu_pair_kernel(SiuArgs a, SiuA
       for (int j = 0; j < MAXT; ++j) {
         const int task = tid + j * NT;
         const int g = min(max(rb + task / QPP, 0), HH - 1);
-        pre[j] = ld4(rx, (uint32_t)g * (C * 4u) + ci * 4u);
+        if constexpr (POOL) {
+          const uint32_t cl = tdiv((uint32_t)g, tm, ts);
+          const int tt = g - (int)cl * a.t;
+          const uint32_t src = ((uint32_t)cl * (uint32_t)p.t_src + 2u * tt) * (CIN * 4u) + ci * 4u;
+          const float4 v = ld4(rx, src);
+          const float4 u = ld4(rx, 2 * tt + 1 < p.t_src ? src + CIN * 4u : src);
+          pre[j] = make_float4(fmaxf(v.x, u.x), fmaxf(v.y, u.y), fmaxf(v.z, u.z), fmaxf(v.w, u.w));
+        } else {
+          pre[j] = ld4(rx, (uint32_t)g * (C * 4u) + ci * 4u);
+        }
       }
 #pragma unroll
       for (int j = 0; j < MAXT; ++j) {
@@ -457,7 +491,6 @@ __global__ void __launch_bounds__(64 * NW, MINW) siu_pair_kernel(SiuArgs a, SiuA
   }
 
   constexpr int kstride = (C / 32) * 512;
-  constexpr int tap_stride = C * NCH * CK;
   const int lofs = wn * 512 + lane * 8;
   int mrow[MT], trow[MT], grow[MT];   // per tile: this lane's row i, its position in its clip, rb + i
 #pragma unroll
@@ -467,15 +500,18 @@ __global__ void __launch_bounds__(64 * NW, MINW) siu_pair_kernel(SiuArgs a, SiuA
     const uint32_t gp = (uint32_t)(grow[mt] + a.t);
     trow[mt] = (int)(gp - tdiv(gp, tm, ts) * (uint32_t)a.t);
   }
-  // acc = W^T X^T over LDS rows (row i's taps: LDS rows i .. i + 2, or the zero row)
-  auto gemm = [&](const uint16_t* wh, const uint16_t* wl, f32x16 (&acc)[MT]) {
+  // acc = W^T X^T over LDS rows, NCHK 32-channel chunks (row i's taps: LDS rows i .. i + 2, or the
+  // zero row)
+  auto gemm = [&](auto nchk_c, const uint16_t* wh, const uint16_t* wl, f32x16 (&acc)[MT]) {
+    constexpr int NCHK = decltype(nchk_c)::value;
+    constexpr int tap_stride = C * NCHK * CK;
     const __amdgpu_buffer_rsrc_t rwh = siu_rsrc(wh), rwl = siu_rsrc(wl);
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
       for (int i = 0; i < 16; ++i) acc[mt][i] = 0.0f;
 #pragma unroll 1
-    for (int ch = 0; ch < NCH; ++ch) {
+    for (int ch = 0; ch < NCHK; ++ch) {
 #pragma unroll 1
       for (int tap = 0; tap < TAPS; ++tap) {
         f16x8 bh[KS], bl[KS];
@@ -500,8 +536,8 @@ __global__ void __launch_bounds__(64 * NW, MINW) siu_pair_kernel(SiuArgs a, SiuA
       }
     }
   };
-  // LDS row i + 1 = split(max(fma(v, s16, t16), 0)) of each tile's row, v = fma(acc, u, bias) or the
-  // values themselves (P < 0); rows outside [lo, NR - lo) or the batch stay out of the range guard
+  // LDS row i + 1 = split(max(fma(v, s16, t16), 0)) of each tile's row; rows outside [lo, NR - lo)
+  // or the batch stay out of the range guard
   auto put = [&](const float (&v)[MT][16], int ps, int pt, int lo) {
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
@@ -521,7 +557,7 @@ __global__ void __launch_bounds__(64 * NW, MINW) siu_pair_kernel(SiuArgs a, SiuA
       if (mrow[mt] >= lo && mrow[mt] < NR - lo && grow[mt] >= 0 && grow[mt] < HH) rmax = fmaxf(rmax, tmax);
     }
   };
-  // v = fma(acc, u, bias[pb]) (+ r)
+  // v = fma(acc, u, bias[pb])
   auto unscale = [&](const f32x16 (&acc)[MT], float u, int pb, float (&v)[MT][16]) {
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
@@ -535,55 +571,120 @@ __global__ void __launch_bounds__(64 * NW, MINW) siu_pair_kernel(SiuArgs a, SiuA
       }
   };
 
+  // y = fma(acc, u, bias[pb]) + y (the unit's epilogue: conv + residual, in that order)
+  auto unscale_add = [&](const f32x16 (&acc)[MT], float u, int pb, float (&y)[MT][16]) {
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 bq = *reinterpret_cast<const float4*>(spar + pb * C + wn * 32 + 8 * q + h4);
+        y[mt][4 * q] = fmaf(acc[mt][4 * q], u, bq.x) + y[mt][4 * q];
+        y[mt][4 * q + 1] = fmaf(acc[mt][4 * q + 1], u, bq.y) + y[mt][4 * q + 1];
+        y[mt][4 * q + 2] = fmaf(acc[mt][4 * q + 2], u, bq.z) + y[mt][4 * q + 2];
+        y[mt][4 * q + 3] = fmaf(acc[mt][4 * q + 3], u, bq.w) + y[mt][4 * q + 3];
+      }
+  };
+
   f32x16 acc[MT];
   float v[MT][16];
+  float y[MT][16];   // the running residual: each unit's output
   __syncthreads();
-  // unit a: t1 (rows 1 .. NR - 2 right)
-  gemm(a.wah, a.wal, acc);
+  if constexpr (POOL) {
+    // the pool unit: t1, then y1 = conv_b + the shortcut Conv1D(1, stride 2) of the raw x (siu_kernel's
+    // arithmetic; the shortcut first, into y, while GEMM a's accumulators are dead)
+    gemm(std::integral_constant<int, NCHX>{}, p.wah, p.wal, acc);
+    __syncthreads();
+    unscale(acc, p.ua, 14, v);
+    put(v, 15, 16, 1);
+    const __amdgpu_buffer_rsrc_t rsh = siu_rsrc(p.wsh), rsl = siu_rsrc(p.wsl);
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      f32x16 sacc;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) sacc[i] = 0.0f;
+      const int gs = min(max(grow[mt], 0), HH - 1);
+      const uint32_t cl = tdiv((uint32_t)gs, tm, ts);
+      const int tt = gs - (int)cl * a.t;
+      const uint32_t sxo = ((uint32_t)cl * (uint32_t)p.t_src + 2u * tt) * (CIN * 4u) + koff * 4u;
+#pragma unroll
+      for (int s = 0; s < CIN / 16; ++s) {
+        const f16x8 sbh = ldw(rsh, lofs, s * kstride);
+        const f16x8 sbl = ldw(rsl, lofs, s * kstride);
+        const float4 x0 = ld4(rx, sxo + 64u * s), x1 = ld4(rx, sxo + 64u * s + 16u);
+        const float xv[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+        f16x8 xh, xl;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float w = xv[k] * ACT_SCALE;
+          rbad |= !(fabsf(w) < SPLIT_MAX) ? 1 : 0;
+          xh[k] = (_Float16)w;
+          xl[k] = (_Float16)(w - (float)xh[k]);
+        }
+        sacc = __builtin_amdgcn_mfma_f32_32x32x16_f16(sbl, xh, sacc, 0, 0, 0);
+        sacc = __builtin_amdgcn_mfma_f32_32x32x16_f16(sbh, xl, sacc, 0, 0, 0);
+        sacc = __builtin_amdgcn_mfma_f32_32x32x16_f16(sbh, xh, sacc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 bs = *reinterpret_cast<const float4*>(spar + 18 * C + wn * 32 + 8 * q + h4);
+        y[mt][4 * q] = fmaf(sacc[4 * q], p.us, bs.x);
+        y[mt][4 * q + 1] = fmaf(sacc[4 * q + 1], p.us, bs.y);
+        y[mt][4 * q + 2] = fmaf(sacc[4 * q + 2], p.us, bs.z);
+        y[mt][4 * q + 3] = fmaf(sacc[4 * q + 3], p.us, bs.w);
+      }
+      // evaluate this tile's range tests here: left to the compiler, they sink to the kernel's end
+      // and keep every scaled shortcut operand alive across the chain (hundreds of spilled VGPRs)
+      asm volatile("" : "+v"(rbad));
+      __builtin_amdgcn_sched_barrier(0);   // one tile's shortcut operands live at a time
+    }
+    __syncthreads();
+    gemm(std::integral_constant<int, NCH>{}, p.wbh, p.wbl, acc);
+    unscale_add(acc, p.ub, 17, y);
+    __syncthreads();   // every wave has read t1
+    put(y, 12, 13, 2);
+    __syncthreads();
+  } else {
+    // the raw x of each tile row: the first unit's residual, loaded under its GEMMs
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int g = min(max(grow[mt], 0), HH - 1);
+        const float4 r = ld4(rx, (uint32_t)g * (C * 4u) + (wn * 32 + 8 * q + h4) * 4u);
+        y[mt][4 * q] = r.x;
+        y[mt][4 * q + 1] = r.y;
+        y[mt][4 * q + 2] = r.z;
+        y[mt][4 * q + 3] = r.w;
+      }
+  }
+  // unit a
+  gemm(std::integral_constant<int, NCH>{}, a.wah, a.wal, acc);
   __syncthreads();
   unscale(acc, a.ua, 0, v);
-  put(v, 1, 2, 1);
-  // y2 = x + conv_b (rows 2 .. NR - 3 right): the raw x of each tile row, loaded under GEMM b
-  float y2[MT][16];
-#pragma unroll
-  for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int g = min(max(grow[mt], 0), HH - 1);
-      const float4 r = ld4(rx, (uint32_t)g * (C * 4u) + (wn * 32 + 8 * q + h4) * 4u);
-      y2[mt][4 * q] = r.x;
-      y2[mt][4 * q + 1] = r.y;
-      y2[mt][4 * q + 2] = r.z;
-      y2[mt][4 * q + 3] = r.w;
-    }
+  put(v, 1, 2, P0 + 1);
   __syncthreads();
-  gemm(a.wbh, a.wbl, acc);
-  unscale(acc, a.ub, 3, v);
-#pragma unroll
-  for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) y2[mt][r] = v[mt][r] + y2[mt][r];
+  gemm(std::integral_constant<int, NCH>{}, a.wbh, a.wbl, acc);
+  unscale_add(acc, a.ub, 3, y);
   __syncthreads();   // every wave has read t1
-  // unit b: its staged input, then t1 (rows 3 .. NR - 4 right), then the output (rows 4 .. NR - 5)
-  put(y2, 4, 5, 2);
+  // unit b
+  put(y, 4, 5, P0 + 2);
   __syncthreads();
-  gemm(b.wah, b.wal, acc);
+  gemm(std::integral_constant<int, NCH>{}, b.wah, b.wal, acc);
   __syncthreads();
   unscale(acc, b.ua, 6, v);
-  put(v, 7, 8, 3);
+  put(v, 7, 8, P0 + 3);
   __syncthreads();
-  gemm(b.wbh, b.wbl, acc);
-  unscale(acc, b.ub, 9, v);
+  gemm(std::integral_constant<int, NCH>{}, b.wbh, b.wbl, acc);
+  unscale_add(acc, b.ub, 9, y);
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
     const int i = mrow[mt], g = grow[mt];
-    const bool ok = i >= 4 && i < NR - 4 && g < HH;
+    const bool ok = i >= F && i < F + RO && g < HH;
     if constexpr (!FIN) {
       if (ok) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const float4 val = make_float4(v[mt][4 * q] + y2[mt][4 * q], v[mt][4 * q + 1] + y2[mt][4 * q + 1],
-                                         v[mt][4 * q + 2] + y2[mt][4 * q + 2], v[mt][4 * q + 3] + y2[mt][4 * q + 3]);
+          const float4 val = make_float4(y[mt][4 * q], y[mt][4 * q + 1], y[mt][4 * q + 2], y[mt][4 * q + 3]);
           *reinterpret_cast<float4*>(b.y + (size_t)g * C + wn * 32 + 8 * q + h4) = val;
         }
       }
@@ -599,8 +700,7 @@ __global__ void __launch_bounds__(64 * NW, MINW) siu_pair_kernel(SiuArgs a, SiuA
         float out[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const float val = v[mt][4 * q + e] + y2[mt][4 * q + e];
-          const int r = __builtin_bit_cast(int, fmaxf(fmaf(val, fsv[e], ftv[e]), 0.0f));
+          const int r = __builtin_bit_cast(int, fmaxf(fmaf(y[mt][4 * q + e], fsv[e], ftv[e]), 0.0f));
           const float r0 = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(r, 0x00, 0xf, 0xf, false));
           const float r1 = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(r, 0x55, 0xf, 0xf, false));
           const float r2 = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(r, 0xaa, 0xf, 0xf, false));
@@ -612,7 +712,7 @@ __global__ void __launch_bounds__(64 * NW, MINW) siu_pair_kernel(SiuArgs a, SiuA
       }
     }
   }
-  if (!(rmax < SPLIT_MAX) && a.range_flag) *a.range_flag = 1;
+  if ((rbad || !(rmax < SPLIT_MAX)) && a.range_flag) *a.range_flag = 1;
 }
 
 // q = x / d for x < 2^31 as (umulhi(x, m) + x) >> s: s = ceil(log2 d), m = floor(2^(32+s) / d) + 1 - 2^32
@@ -636,15 +736,17 @@ hipError_t launch(const SiuArgs& a0, hipStream_t s) {
   return hipGetLastError();
 }
 
-template <int C, int NR, int NW, bool FIN, int MINW>
-hipError_t launch_pair(const SiuArgs& a0, const SiuArgs& b, hipStream_t s) {
-  constexpr int RO = NR - 8;
+template <int CIN, int C, int NR, int NW, bool POOL, bool FIN, int MINW>
+hipError_t launch_chain(const SiuArgs& p, const SiuArgs& a0, const SiuArgs& b, hipStream_t s) {
+  constexpr int RO = chain_rows<NR, POOL, FIN>();
   SiuArgs a = a0;
   siu_fastdiv((uint32_t)a.t, a.tdiv_m, a.tdiv_s);
   const int64_t rows = (int64_t)a.n * a.t;
-  if (rows >= (1 << 24) || rows * C * 4 > 0xffffff00ll) return hipErrorInvalidValue;
+  const int64_t xbytes = (int64_t)a.n * (POOL ? p.t_src : a.t) * CIN * 4;
+  if (rows >= (1 << 24) || xbytes > 0xffffff00ll || rows * C * 4 > 0xffffff00ll) return hipErrorInvalidValue;
   const int64_t blocks = (rows + RO - 1) / RO;
-  hipLaunchKernelGGL((siu_pair_kernel<C, NR, NW, FIN, MINW>), dim3((unsigned)blocks), dim3(64 * NW), 0, s, a, b);
+  hipLaunchKernelGGL((siu_chain_kernel<CIN, C, NR, NW, POOL, FIN, MINW>), dim3((unsigned)blocks), dim3(64 * NW), 0,
+                     s, p, a, b);
   return hipGetLastError();
 }
 
@@ -657,12 +759,31 @@ hipError_t siu_pair_launch(const SiuArgs& a, const SiuArgs& b, int c, hipStream_
   if (!a.x || a.n != b.n || a.t != b.t || a.t < 1) return hipErrorInvalidValue;
   if (b.seq) {   // units 8-9 with the final BN + ReLU + AveragePooling1D(4)
     if (!b.fs || !b.ft || a.t % 4 != 0 || c != 128) return hipErrorInvalidValue;
-    return launch_pair<128, 128, 4, true, 2>(a, b, s);
+    return launch_chain<128, 128, 128, 4, false, true, 2>(a, a, b, s);
   }
   if (!b.y || b.y == a.x) return hipErrorInvalidValue;
-  if (c == 32) return launch_pair<32, 256, 4, false, 3>(a, b, s);
-  if (c == 64) return launch_pair<64, 256, 4, false, 2>(a, b, s);
-  if (c == 128) return launch_pair<128, 128, 4, false, 2>(a, b, s);
+  if (c == 32) return launch_chain<32, 32, 256, 4, false, false, 3>(a, a, b, s);
+  if (c == 64) return launch_chain<64, 64, 256, 4, false, false, 2>(a, a, b, s);
+  if (c == 128) return launch_chain<128, 128, 128, 4, false, false, 2>(a, a, b, s);
+  return hipErrorInvalidValue;
+}
+
+bool siu_triple_supported(int cin, int c) { return sipu_supported(cin, c); }
+
+hipError_t siu_triple_launch(const SiuArgs& p, const SiuArgs& a, const SiuArgs& b, int cin, int c,
+                             hipStream_t s) {
+  if ((int64_t)a.n * a.t == 0) return hipSuccess;
+  if (!p.x || !p.wsh || !p.wsl || !p.bs || p.n != a.n || a.n != b.n || p.t != a.t || a.t != b.t || a.t < 1 ||
+      a.t != (p.t_src + 1) / 2)
+    return hipErrorInvalidValue;
+  if (b.seq) {
+    if (!b.fs || !b.ft || a.t % 4 != 0 || cin != 64 || c != 128) return hipErrorInvalidValue;
+    return launch_chain<64, 128, 128, 4, true, true, 2>(p, a, b, s);
+  }
+  if (!b.y || b.y == p.x) return hipErrorInvalidValue;
+  if (cin == 32 && c == 32) return launch_chain<32, 32, 256, 4, true, false, 3>(p, a, b, s);
+  if (cin == 32 && c == 64) return launch_chain<32, 64, 256, 4, true, false, 2>(p, a, b, s);
+  if (cin == 64 && c == 128) return launch_chain<64, 128, 128, 4, true, false, 2>(p, a, b, s);
   return hipErrorInvalidValue;
 }
 

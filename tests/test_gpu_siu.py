@@ -6,7 +6,8 @@ probabilities over a batch with ragged and 'silent' clips, across several tiles 
 * MMLA_NO_SIFIN: the last unit writing the final BN + ReLU + AveragePooling1D(4) itself;
 * MMLA_NO_SIPAD: si_fe's 40-float feature rows (zero 40th column) read by the stem as float4;
 * MMLA_NO_SIPAIR: two consecutive units without pooling as one kernel (the first unit's output kept
-  on chip), with and without the last unit's fused pooling.
+  on chip), with and without the last unit's fused pooling;
+* MMLA_NO_SICHAIN: a pool unit and the two units after it as one kernel.
 Each switch is set explicitly, so the tests hold whatever the library's defaults are."""
 import numpy as np
 import pytest
@@ -16,9 +17,9 @@ from oracle import synth
 pytestmark = pytest.mark.gpu
 
 ALL_ON = {'MMLA_NO_SIU': '0', 'MMLA_NO_SIPU': '0', 'MMLA_NO_SIFIN': '0', 'MMLA_NO_SIPAD': '0',
-          'MMLA_NO_SIPAIR': '0'}
+          'MMLA_NO_SIPAIR': '0', 'MMLA_NO_SICHAIN': '0'}
 ALL_OFF = {'MMLA_NO_SIU': '1', 'MMLA_NO_SIPU': '1', 'MMLA_NO_SIFIN': '1', 'MMLA_NO_SIPAD': '1',
-           'MMLA_NO_SIPAIR': '1'}
+           'MMLA_NO_SIPAIR': '1', 'MMLA_NO_SICHAIN': '1'}
 
 
 def _ctx(monkeypatch, env):
@@ -63,8 +64,14 @@ def test_padded_feature_rows_bit_identical(monkeypatch, pcm):
 
 
 def test_unit_pairs_bit_identical(monkeypatch, pcm):
-    _same(monkeypatch, pcm, ALL_ON, dict(ALL_ON, MMLA_NO_SIPAIR='1'))
-    _same(monkeypatch, pcm, dict(ALL_ON, MMLA_NO_SIFIN='1'), dict(ALL_ON, MMLA_NO_SIPAIR='1', MMLA_NO_SIFIN='1'))
+    no_chain = dict(ALL_ON, MMLA_NO_SICHAIN='1')
+    _same(monkeypatch, pcm, no_chain, dict(no_chain, MMLA_NO_SIPAIR='1'))
+    _same(monkeypatch, pcm, dict(no_chain, MMLA_NO_SIFIN='1'), dict(no_chain, MMLA_NO_SIPAIR='1', MMLA_NO_SIFIN='1'))
+
+
+def test_unit_chains_bit_identical(monkeypatch, pcm):
+    _same(monkeypatch, pcm, ALL_ON, dict(ALL_ON, MMLA_NO_SICHAIN='1'))
+    _same(monkeypatch, pcm, dict(ALL_ON, MMLA_NO_SIFIN='1'), dict(ALL_ON, MMLA_NO_SICHAIN='1', MMLA_NO_SIFIN='1'))
 
 
 @pytest.mark.parametrize('n', [1, 2, 5])

@@ -18,7 +18,7 @@ for r in csv.DictReader(open(sys.argv[1])):
         if 'siu' in n:
             tot += float(r['TotalDurationNs']) / 1e6
 d = json.loads([l for l in open('gpurun_out/ks_s.json') if l.startswith('{')][0])
-print('siu total ms', round(tot, 3), 'value', round(d['value']), 'conv frac', round(d['roofline']['frac'], 4),
+print('siu total ms', round(tot, 3), 'value', round(d['value']), 'roof', d['roofline']['kernel'], round(d['roofline']['frac'], 4), 'conv frac', round((d.get('roofline_conv') or d['roofline'])['frac'], 4),
       'parity', d['parity'])
 PY
 done
