@@ -115,6 +115,10 @@ __global__ void __launch_bounds__(64 * NW, MINW) odu_kernel(OduArgs a) {
   const int64_t clip = bid / TLW;
   const int w0 = (int)(bid - clip * TLW) * TW;
   const float* __restrict__ xc = a.x + clip * ((int64_t)H * W * CIN);
+  // the clip's input through a buffer descriptor: out-of-image halo pixels read zeros with no branch
+  // around the load (a load inside a divergent branch is waited for inside it)
+  const __amdgpu_buffer_rsrc_t rxc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(xc), (short)0,
+                                                                       (int)(H * W * CIN * 4), 0x00020000);
   const int koff = (lane >> 5) * 8;
   const int hsel = 4 * (lane >> 5);
   const int cob = wn * 32;                    // this wave's output-channel tile
@@ -150,13 +154,12 @@ __global__ void __launch_bounds__(64 * NW, MINW) odu_kernel(OduArgs a) {
 #pragma unroll
       for (int j = 0; j < MAXT; ++j) {
         const int task = tid + j * NT;
-        pre[j] = make_float4(0.f, 0.f, 0.f, 0.f);
         const int px = task / QPP;
         const int ih = px / XP - 1, iw = w0 + px % XP - 1;
-        if (task < NXP * QPP && ih >= 0 && ih < H && iw >= 0 && iw < W) {
-          pre[j] = *reinterpret_cast<const float4*>(xc + ((int64_t)ih * W + iw) * CIN + ci);
-          valid |= 1u << j;
-        }
+        const bool ok = task < NXP * QPP && ih >= 0 && ih < H && iw >= 0 && iw < W;
+        pre[j] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                rxc, ok ? (uint32_t)((ih * W + iw) * CIN + ci) * 4u : 0x80000000u, 0, 0));
+        valid |= (uint32_t)ok << j;
       }
 #pragma unroll
       for (int j = 0; j < MAXT; ++j) {
@@ -288,8 +291,8 @@ __global__ void __launch_bounds__(64 * NW, MINW) odu_kernel(OduArgs a) {
       const bool ok = w0 + c < W;
 #pragma unroll
       for (int qd = 0; qd < 4; ++qd)
-        rsd[mt][qd] = ok ? *reinterpret_cast<const float4*>(xc + ((int64_t)i * W + w0 + c) * C + cob + 8 * qd + hsel)
-                         : make_float4(0.f, 0.f, 0.f, 0.f);
+        rsd[mt][qd] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
+                          rxc, ok ? (uint32_t)((i * W + w0 + c) * C + cob + 8 * qd + hsel) * 4u : 0x80000000u, 0, 0));
     }
   }
 #pragma unroll
