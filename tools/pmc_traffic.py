@@ -10,7 +10,7 @@ from collections import defaultdict
 
 STAGE = {  # kernel-name substring -> bench stage (mmla.h MMLA_STAGE_*)
     'resblk_kernel': 'conv', 'rbs_kernel': 'conv', 'conv_h3_kernel': 'conv', 'conv_kernel': 'conv', 'odu_kernel': 'conv',
-    'siu_kernel': 'conv', 'siu_pair_kernel': 'conv',
+    'siu_kernel': 'conv', 'siu_pair_kernel': 'conv', 'siu_chain_kernel': 'conv',
     'od_fe_kernel': 'od_fe', 'od_fe3_kernel': 'od_fe', 'si_fe_kernel': 'si_fe', 'bilstm_kernel': 'lstm',
     'bilstm_h3_kernel': 'lstm',
 }
