@@ -202,6 +202,19 @@ MMLA_DEV void for_tiles(F&& f, std::integer_sequence<int, I...>) {
 // writes, A reads; Z: A / B; P: B / A; sgn: B / A; cnt: A / B; zc: double-buffered by clip).  The
 // five tiles of a clip are unrolled (tile-dependent edges, offsets and dB register slots become
 // compile-time); the loop runs over the workgroup's clips plus one drain pass.
+#ifndef FE_TRACE
+#define FE_TRACE 0
+#endif
+#if FE_TRACE
+// dev phase timeline (FE_TRACE builds only, tools/fe_timeline.py): s_memtime at 8 points of every
+// tile step of the third clip of the first 256 workgroups, per wave
+__device__ unsigned long long fe_trace_buf[256 * 16 * 5 * 8];
+#define FE_T(i) do { if (trace_on) tt[i] = __builtin_amdgcn_s_memtime(); } while (0)
+#define FE_TFLUSH(t) do { if (trace_on && lane == 0) { for (int i_ = 0; i_ < 8; ++i_) fe_trace_buf[(((size_t)blockIdx.x * 16 + wid) * 5 + (t)) * 8 + i_] = tt[i_]; } } while (0)
+#else
+#define FE_T(i) do { } while (0)
+#define FE_TFLUSH(t) do { } while (0)
+#endif
 template <bool DB, bool NM, bool IMG>
 __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_clips) {
   __shared__ __attribute__((aligned(16))) Smem sm;
@@ -695,19 +708,28 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
           mel(tile_c<NTILE - 1>{}, p_r);
         }
       };
+#if FE_TRACE
+      const bool trace_on = ci == 2 && blockIdx.x < 256;
+      unsigned long long tt[8];
+#endif
+      FE_T(0);
       // ---- interval A ----
       if (cur) {
         crossings(T_);
         stage1(r, hh);
       }
+      FE_T(1);
       if (t == 1 && ci > 0) {   // the previous clip: its last mel and max / min finished in step 0
         epilogue(clip - gridDim.x, par ^ 1);
       }
+      FE_T(2);
       __syncthreads();
+      FE_T(3);
       if (!cur && t == 1) return;
       // ---- interval B ----  (the mel of tile t - 1 first: its MFMAs then start on every wave at the
       // barrier instead of queueing behind stage 2's on waves 0-12 -- 0.2975 -> 0.2903 ms, A/B)
       mel_prev();   // (after the epilogue: tile 0's mel overwrites the dB registers it read)
+      FE_T(4);
       if (t == 0 && ci > 0) {
         const float mx = wave_red<true>(smax), mn = wave_red<false>(smin);
         if (lane == 0) {
@@ -718,6 +740,7 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
         smin = INFINITY;
       }
       if (cur) stage2(r, hh, p_w);
+      FE_T(5);
       if (cur) {
         zsum(T_, par);
         if constexpr (t + 1 < NTILE) {
@@ -731,7 +754,10 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
           prefetch(ci + 1 < my_clips ? clip + gridDim.x : n_clips, tile_c<t + 2 - NTILE>{});
         }
       }
+      FE_T(6);
       __syncthreads();
+      FE_T(7);
+      FE_TFLUSH(t);
     }, std::make_integer_sequence<int, NTILE>{});
   }
   if (fbad && a.range_flag) *a.range_flag = 1;
@@ -740,6 +766,12 @@ __global__ void __launch_bounds__(NTH, 1) od_fe3_kernel(OdFeArgs a, int64_t n_cl
 }  // namespace v3
 
 }  // namespace
+
+#if FE_TRACE
+extern "C" int mmla_debug_fe_trace(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(v3::fe_trace_buf), sizeof(v3::fe_trace_buf)) == hipSuccess ? 0 : -2;
+}
+#endif
 
 bool od_fe_tables_ok(const OdFeTables& t) {
   for (int m = 0; m < 128; ++m) {
