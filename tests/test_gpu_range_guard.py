@@ -177,3 +177,21 @@ def test_float_pcm_outside_split_range():
         c.synchronize()
     assert e.value.code == _lib.MMLA_E_RANGE
     c.synchronize()
+
+
+@pytest.mark.parametrize('bn', [3, 6, 12, 36])
+def test_si_chain_overflow_host_call_reruns_in_f32(bn):
+    """every split inside the fused SI res-unit chains (siu.hip siu_chain_kernel) is range-guarded:
+    a BatchNorm scaled past the fp16 range in the pool unit's t1 (lww-3), the second unit's input
+    (lww-6), the third unit's t1 (lww-12) or the last chain's unit 9 input (lww-36) flags the launch,
+    and the host call re-runs the micro-batch in exact f32"""
+    from mmla_audio_amd import _lib, weights
+    W = weights.synthetic(weights.SI, seed=8, n_classes=8)
+    W[f'layer_with_weights-{bn}/gamma'] = W[f'layer_with_weights-{bn}/gamma'] * 1.0e5
+    W[f'layer_with_weights-{bn}/beta'] = np.abs(W[f'layer_with_weights-{bn}/beta']) * 1.0e5
+    pcm = synth.batch(350 + bn, 6, 24000)
+    c = _ctx(W_si=W)
+    p, a, _ = c.si_pipeline(pcm)
+    assert c.range_check() >= 1
+    p32, a32, _ = _ctx(W_si=W, prec=_lib.PREC_F32).si_pipeline(pcm)
+    assert np.array_equal(p, p32) and np.array_equal(a, a32)
