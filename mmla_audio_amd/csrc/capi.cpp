@@ -136,7 +136,8 @@ struct mmla_ctx {
   // unit writes its output and bn_relu_avgpool4 runs as its own launch
   bool sifin = true;
   // ... and two consecutive units without pooling (2-3, 5-6, 8-9) as one kernel (siu.hip
-  // siu_pair_kernel: the first unit's output stays on chip); env MMLA_NO_SIPAIR=1: one launch each
+  // siu_chain_kernel without a pool unit: the first unit's output stays on chip); env MMLA_NO_SIPAIR=1:
+  // one launch each
   bool sipair = true;
   // ... and a pool unit with the two units after it (1-3, 4-6, 7-9) as one kernel (siu.hip
   // siu_chain_kernel POOL); env MMLA_NO_SICHAIN=1: the pool unit alone, then the pair
