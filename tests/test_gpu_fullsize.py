@@ -1,5 +1,6 @@
-"""Full-size batches (BASELINE configs 3 and 4): every clip of a >= 2-micro-batch OD run and a
-65 536-clip SI run equals its batch-1 result, clips are compared at every micro-batch edge (the
+"""Full-size batches (BASELINE configs 3 and 4): every sampled clip of a 65 573-clip OD run (config
+3's 65 536 clips + a partial micro-batch; exact f32: two micro-batches + 37) and a 65 536-clip SI run
+equals its batch-1 result, clips are compared at every micro-batch edge (the
 OD activation buffers exceed 2^31 elements there, so a 32-bit index anywhere would show), and a
 sample matches the oracle to |log p - log p_ref| <= 1e-4 with identical argmax (oracle/compare.py).
 
@@ -33,7 +34,8 @@ def test_od_two_microbatches(prec):
     c.load_weights(weights.OD, weights.pack(weights.OD, W), 2)
     c.set_precision(_lib.PREC_F16X3 if prec == 'f16x3' else _lib.PREC_F32)
     mb = c.get_microbatch()[0]
-    n = 2 * mb + 37          # two full micro-batches and a partial third
+    # config 3 (65 536 clips) and a partial micro-batch after it; exact f32: two + a partial third
+    n = max(65536, 4 * mb) + 37 if prec == 'f16x3' else 2 * mb + 37
     pcm = make_clips(n, 40000, start_index=50000)
     probs = torch.empty((n, 2), dtype=torch.float32, device='cuda')
     am = torch.empty(n, dtype=torch.int32, device='cuda')
